@@ -1,0 +1,261 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident RFC 1071 checksum of synthetic packet batches on
+MI355X (BASELINE.json metric "GiB/s payload checksummed (device-resident),
+1472 B pkts; % of HBM-read peak").
+
+One step = one pass of the hot path (one wc_cksum_* launch) over one batch
+that is already resident in HBM.  Default workload = BASELINE configs[1] (C2):
+2^20 packets x 1472 B per GPU, stride 1472, splitmix64 bytes.  With --gpus N
+(one process per GPU, torchrun) every rank checksums its own C2 batch: the
+path shards by packet with no data-path collective ("scaling": "weak"); ranks
+meet only at the barriers around the timed region and in the max-over-ranks
+time reduction.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4]
+                    [--len L] [--cpu-seconds S] [--no-cpu-baseline]
+
+Rank 0 prints ONE JSON line (see DESIGN.md section 6 for every field).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+METRIC = "GiB/s payload checksummed (device-resident), 1472 B pkts; % of HBM-read peak"
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
+GIB = float(1 << 30)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4"])
+    ap.add_argument("--len", type=int, default=1472, help="packet bytes for c3")
+    ap.add_argument("--packets", type=int, default=1 << 20)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-file", default=str(ROOT / "profiles" / "traffic.json"))
+    return ap.parse_args()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and "WORLD_SIZE" in os.environ:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    pg = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world,
+                                device_id=torch.device("cuda", local))
+        pg = dist
+    return rank, local, world, pg
+
+
+def barrier(pg, dev):
+    torch.cuda.synchronize(dev)
+    if pg is not None:
+        pg.barrier()
+    torch.cuda.synchronize(dev)
+
+
+def max_over_ranks(pg, dev, x: float) -> float:
+    if pg is None:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    pg.all_reduce(t, op=pg.ReduceOp.MAX)
+    return float(t.item())
+
+
+def make_workload(args, dev, rank):
+    import warpcore_amd as wc
+    from warpcore_amd import synth
+
+    seed = synth.SEED + rank
+    if args.config in ("c2", "c3"):
+        L = 1472 if args.config == "c2" else args.len
+        n = args.packets
+        nbytes = n * L
+        buf = torch.empty(nbytes + 64, dtype=torch.uint8, device=dev)
+        wc.synth_fill(buf, seed, nbytes=nbytes)
+        out = torch.empty(n, dtype=torch.uint16, device=dev)
+
+        def step():
+            wc.cksum_strided(buf, L, L, n, out=out)
+
+        plan = wc.plan_strided(buf.data_ptr(), L, L, n)
+        desc = (f"C2: {n} x {L} B packets, stride {L}, device-resident"
+                if args.config == "c2" else f"C3: {n} x {L} B packets, stride {L}")
+        meta = {"packets_per_gpu": n, "packet_bytes": L, "layout": "strided"}
+        return step, n, nbytes, buf, out, plan, desc, meta, (L, L)
+    # C4: Zipf(1) lengths 64..1472 B, packed with no padding (unaligned starts)
+    n = 1 << 24 if args.packets == (1 << 20) else args.packets
+    lens = synth.zipf_lengths(n, seed=synth.ZIPF_SEED + rank)
+    offs = synth.packed_offsets(lens)
+    nbytes = int(lens.astype(np.uint64).sum())
+    buf = torch.empty(nbytes + 64, dtype=torch.uint8, device=dev)
+    wc.synth_fill(buf, seed, nbytes=nbytes)
+    d_off = torch.from_numpy(offs).to(dev)
+    d_len = torch.from_numpy(lens).to(dev)
+    out = torch.empty(n, dtype=torch.uint16, device=dev)
+
+    def step():
+        wc.cksum_ragged(buf, d_off, d_len, out=out)
+
+    desc = f"C4: {n} packets, Zipf(s=1) lengths 64-1472 B (mean {nbytes / n:.1f}), packed"
+    meta = {"packets_per_gpu": n, "mean_packet_bytes": round(nbytes / n, 2),
+            "layout": "ragged"}
+    return step, n, nbytes, buf, out, {"group": 16, "chunks_per_lane": 2, "unroll": 2}, \
+        desc, meta, (offs, lens)
+
+
+def cpu_baseline(args, buf, shape, nbytes_total):
+    """The oracle's C restatement timed on this host's cores (bounded sample)."""
+    from oracle import c_oracle  # checker / baseline only
+
+    threads = c_oracle.default_threads()
+    if args.config in ("c2", "c3"):
+        L, stride = shape
+        n_s = max(1, min(args.packets, (96 << 20) // L))
+        sample = buf[: n_s * stride].cpu().numpy()
+        bps, passes = c_oracle.bench_strided(sample, stride, L, n_s, kind=0,
+                                             threads=threads, min_seconds=args.cpu_seconds)
+        desc = f"first {n_s} packets x {L} B ({n_s * L / 1e6:.0f} MB), {passes} passes"
+    else:
+        offs, lens = shape
+        n_s = min(offs.size, 400000)
+        end = int(offs[n_s - 1]) + int(lens[n_s - 1])
+        sample = buf[:end].cpu().numpy()
+        t0 = time.perf_counter()
+        passes = 0
+        while True:
+            c_oracle.cksum_ragged(sample, offs[:n_s], lens[:n_s], kind=0, threads=threads)
+            passes += 1
+            if time.perf_counter() - t0 >= args.cpu_seconds:
+                break
+        bps = passes * float(lens[:n_s].astype(np.uint64).sum()) / (time.perf_counter() - t0)
+        desc = f"first {n_s} Zipf packets ({end / 1e6:.0f} MB), {passes} passes"
+    try:
+        model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo")
+                     if l.startswith("model name"))
+    except (OSError, StopIteration):
+        model = "unknown"
+    return {"value": round(bps / GIB, 3), "unit": "GiB/s", "cores": threads,
+            "kind": "port", "sample": f"{desc}; oracle/wc_oracle.c -Ofast -march=native, "
+            f"one call per packet, {threads} pthreads on {model}"}
+
+
+def parity_sample(args, buf, out, shape):
+    """Bit-exact check of the last step's results on a sample of packets."""
+    from oracle import c_oracle
+    got = out.cpu().numpy().view(np.uint16)
+    if args.config in ("c2", "c3"):
+        L, stride = shape
+        n_s = min(args.packets, 65536)
+        want = c_oracle.cksum_strided(buf[: n_s * stride].cpu().numpy(), stride, L, n_s, kind=0)
+    else:
+        offs, lens = shape
+        n_s = min(offs.size, 65536)
+        end = int(offs[n_s - 1]) + int(lens[n_s - 1])
+        want = c_oracle.cksum_ragged(buf[:end].cpu().numpy(), offs[:n_s], lens[:n_s], kind=0)
+    return {"checked_packets": int(n_s), "mismatches": int((got[:n_s] != want).sum())}
+
+
+def main():
+    args = parse()
+    rank, local, world, pg = dist_setup(args)
+    dev = torch.device("cuda", local)
+    import warpcore_amd as wc
+    wc.gpu_init(local)
+
+    step, n, nbytes, buf, out, plan, desc, meta, shape = make_workload(args, dev, rank)
+
+    for _ in range(args.warmup):
+        step()
+    barrier(pg, dev)
+
+    stream = torch.cuda.current_stream(dev)  # the stream every launch goes to
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    barrier(pg, dev)
+    elapsed = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps
+
+    elapsed = max_over_ranks(pg, dev, elapsed)
+    kernel_ms_max = max_over_ranks(pg, dev, kernel_ms)
+    total_bytes = float(nbytes) * world * args.steps
+    value = total_bytes / elapsed / GIB
+    achieved = nbytes / (kernel_ms * 1e-3) / 1e9  # GB/s of payload per launch (rank-local)
+
+    parity = parity_sample(args, buf, out, shape)
+    if pg is not None:
+        t = torch.tensor([parity["mismatches"]], dtype=torch.int64, device=dev)
+        pg.all_reduce(t)
+        parity["mismatches"] = int(t.item())
+
+    traffic = None
+    try:
+        tf = json.loads(Path(args.traffic_file).read_text())
+        key = f"{args.config}:{meta.get('packet_bytes', 'zipf')}"
+        if key in tf:
+            traffic = tf[key]["hbm_bytes_per_launch"]
+    except (OSError, ValueError, KeyError):
+        traffic = None
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, buf, shape, nbytes)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic: splitmix64 payload bytes generated on device (wc_synth_fill)",
+            "config": {"workload": desc, **meta, "parallelism": f"packet-shard x{world}",
+                       "kernel_shape": plan, "payload_GBps": round(value * GIB / 1e9, 1)},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
+                         "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                         "traffic": traffic,
+                         "kernel_ms_avg": round(kernel_ms, 5),
+                         "kernel_ms_avg_max_rank": round(kernel_ms_max, 5)},
+            "cpu_baseline": cpu,
+            "parity": parity,
+        }
+        print(json.dumps(line), flush=True)
+    if pg is not None:
+        pg.barrier()
+        pg.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,120 @@
+/*
+ * wc_cksum.h -- C ABI of the MI355X (gfx950) Internet / UDP checksum library
+ * (libwccksum.so).  Plain C types only; every device-side pointer is a HIP
+ * device (or mapped pinned host) address, every `stream` is a hipStream_t
+ * passed as void* (NULL = the legacy default stream).
+ *
+ * Drop-in boundary.  The reference exposes exactly two checksum entry points,
+ * declared at /root/reference/lib/src/in_cksum.h:32-36 and defined at
+ * /root/reference/lib/src/in_cksum.c:133-167:
+ *
+ *     uint16_t ip_cksum(const void *buf, uint16_t len);
+ *     uint16_t payload_cksum(const void *buf, uint16_t len);
+ *
+ * This library exports both under the same names and with the same semantics
+ * (bit-identical results, no error channel, result stored raw into the
+ * packet), computed on the GPU.  Around them it adds the batch entry points
+ * the reference's per-packet loops would call at their natural batch points
+ * (w_tx's sq_foreach, backend_netmap.c:348-358, and the RX ring drain,
+ * backend_netmap.c:379-391); see INTEGRATION.md.
+ *
+ * Return convention of the int-returning functions: 0 on success, a negative
+ * WC_E* code on a caller error, or -(int)hipError_t on a HIP runtime error.
+ */
+#pragma once
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Which reference function each packet is checksummed with. */
+enum wc_cksum_kind {
+    WC_CKSUM_IP = 0,      /* ip_cksum(buf, len)       in_cksum.c:133-137 */
+    WC_CKSUM_PAYLOAD = 1, /* payload_cksum(buf, len)  in_cksum.c:140-167 */
+};
+
+/* Library error codes (HIP errors are returned as -(int)hipError_t, which
+ * never collides with these). */
+#define WC_OK 0
+#define WC_EINVAL (-10001)   /* bad argument (NULL pointer, bad kind, ...) */
+#define WC_ENODEV (-10002)   /* no usable gfx950 device */
+#define WC_ENOMEM (-10003)   /* scratch / staging allocation failed */
+
+/* --- drop-in scalar entry points (reference in_cksum.h:32-36) ------------ */
+
+/* Same contract as the reference: `buf` is host memory owned by the caller
+ * (a netmap slot or w_iov buffer), read only; the return value is the
+ * checksum as a native uint16 whose in-memory bytes are the network-order
+ * checksum.  There is no error channel -- like the reference's ensure()/die()
+ * (util.h:280-340) an unusable GPU aborts the process with a message. */
+uint16_t ip_cksum(const void *buf, uint16_t len);
+uint16_t payload_cksum(const void *buf, uint16_t len);
+
+/* --- device-resident batch entry points ---------------------------------- */
+
+/* Packet i occupies [base + i*stride, base + i*stride + len).  Any alignment
+ * and any stride (including stride < len, overlapping) is accepted.
+ * out[i] receives the checksum of packet i (device memory, n entries). */
+int wc_cksum_strided(const void *d_base, uint64_t stride, uint16_t len,
+                     uint64_t n, uint16_t *d_out, int kind, void *stream);
+
+/* Packet i occupies [base + d_off[i], base + d_off[i] + d_len[i]) (d_off and
+ * d_len are device arrays of n entries).  Any alignment is accepted. */
+int wc_cksum_ragged(const void *d_base, const uint64_t *d_off,
+                    const uint16_t *d_len, uint64_t n, uint16_t *d_out,
+                    int kind, void *stream);
+
+/* RX-side verification (udp.c:132-139, ip4.c:110-115): like the batch calls
+ * above, and additionally counts the packets whose checksum is not 0 into
+ * *d_bad (a device uint64, accumulated, not reset).  d_out may be NULL. */
+int wc_verify_strided(const void *d_base, uint64_t stride, uint16_t len,
+                      uint64_t n, uint16_t *d_out, uint64_t *d_bad, int kind,
+                      void *stream);
+int wc_verify_ragged(const void *d_base, const uint64_t *d_off,
+                     const uint16_t *d_len, uint64_t n, uint16_t *d_out,
+                     uint64_t *d_bad, int kind, void *stream);
+
+/* --- host-memory batch (end-to-end: pinned H2D, kernel, D2H) ------------- */
+
+/* Same as wc_cksum_ragged, but every buffer is host memory: the packet bytes
+ * [h_base, h_base + h_bytes) are streamed to the GPU in chunks over several
+ * HIP streams with hipMemcpyAsync, and the results come back into h_out.
+ * Synchronous.  Register the buffer first (wc_host_register) to avoid an
+ * extra host copy into the library's pinned staging ring. */
+int wc_cksum_host(const void *h_base, uint64_t h_bytes, const uint64_t *h_off,
+                  const uint16_t *h_len, uint64_t n, uint16_t *h_out, int kind);
+
+/* Page-lock a host region (e.g. the netmap buffer area w->mem,
+ * backend_netmap.c:149-151) so wc_cksum_host can DMA from it directly. */
+int wc_host_register(void *h_ptr, uint64_t bytes);
+int wc_host_unregister(void *h_ptr);
+
+/* --- library lifetime / introspection ------------------------------------ */
+
+/* Select the HIP device for this thread and create the library's scratch
+ * (staging ring, streams).  Called implicitly by every entry point with
+ * device -1 ("current device"); calling it explicitly is optional. */
+int wc_gpu_init(int device);
+/* Release the scratch created by wc_gpu_init. */
+int wc_gpu_fini(void);
+
+/* Counter-based synthetic packet bytes (bench / tests): little-endian 8-byte
+ * word k of [d_buf, d_buf + nbytes) is splitmix64 output k for `seed`. */
+int wc_synth_fill(void *d_buf, uint64_t nbytes, uint64_t seed, void *stream);
+
+/* Kernel-configuration introspection: fills the group width G (lanes per
+ * packet), chunk loads per lane and packets per group-iteration the
+ * dispatcher picks for a strided batch of `len`-byte packets. */
+int wc_plan_strided(uint64_t base_addr, uint64_t stride, uint16_t len,
+                    uint64_t n, int kind, int *group, int *chunks_per_lane,
+                    int *unroll, int *grid);
+
+const char *wc_strerror(int err);
+const char *wc_version(void);
+
+#ifdef __cplusplus
+}
+#endif

@@ -1,0 +1,52 @@
+"""CPU tests of the drop-in boundary: the gfx950 library builds, loads and
+exports exactly the C ABI that include/warpcore_gpu/wc_cksum.h declares
+(no compute calls -- there is no GPU here)."""
+import re
+import subprocess
+from pathlib import Path
+
+from warpcore_amd import _build, _lib
+
+ROOT = Path(__file__).resolve().parent.parent
+HEADER = ROOT / "include" / "warpcore_gpu" / "wc_cksum.h"
+
+
+def declared_functions():
+    text = re.sub(r"/\*.*?\*/", "", HEADER.read_text(), flags=re.S)
+    return set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*([a-z_0-9]+)\s*\(", text, re.M))
+
+
+def exported_symbols(path):
+    out = subprocess.run(["nm", "-D", "--defined-only", str(path)], check=True,
+                         capture_output=True, text=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if " T " in line}
+
+
+def test_header_declares_reference_entry_points():
+    names = declared_functions()
+    # in_cksum.h:32-36 -- the two functions the reference's callers bind.
+    assert {"ip_cksum", "payload_cksum"} <= names
+    assert "wc_cksum_strided" in names and "wc_cksum_ragged" in names
+
+
+def test_library_builds_and_exports_every_declared_symbol():
+    lib = _build.build_lib()
+    exported = exported_symbols(lib)
+    missing = declared_functions() - exported
+    assert not missing, f"declared but not exported: {missing}"
+
+
+def test_python_binding_covers_header():
+    assert declared_functions() == set(_lib.SIGNATURES)
+
+
+def test_ctypes_load():
+    lib = _lib.load()
+    assert lib.wc_version().decode().startswith("wccksum")
+    assert lib.wc_strerror(-10001).decode() == "invalid argument"
+
+
+def test_code_object_targets_gfx950_only():
+    blob = _build.build_lib().read_bytes()
+    targets = set(re.findall(rb"amdgcn-amd-amdhsa-[-a-z0-9:+]*gfx[0-9a-z]+", blob))
+    assert targets == {b"amdgcn-amd-amdhsa--gfx950"}

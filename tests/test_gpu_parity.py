@@ -1,0 +1,266 @@
+"""GPU parity tests: the gfx950 kernels (through the C ABI) against the CPU
+oracle on the same bytes -- bit-exact, every packet.
+
+Sizes: the golden fixtures and edge sweeps are small; the BASELINE.json
+configurations C2 (2^20 x 1472 B), C3 (MTU sweep x 2^20) and C4 (2^24 Zipf
+packets, packed unaligned) are checked in full against the multi-threaded C
+oracle.
+"""
+import json
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+import torch
+
+import warpcore_amd as wc
+from oracle import c_oracle, py_oracle
+from packets import insert_checksum, ipv4_udp, ipv6_udp, pack, random_packets
+from warpcore_amd import synth
+
+pytestmark = pytest.mark.gpu
+GOLDEN = Path(__file__).resolve().parent / "golden"
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def to_dev(a: np.ndarray, dev) -> torch.Tensor:
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def dev_u8(a: np.ndarray, dev, pad: int = 64) -> torch.Tensor:
+    """Device copy with 16-byte aligned base and `pad` spare bytes."""
+    t = torch.zeros(a.size + pad, dtype=torch.uint8, device=dev)
+    t[: a.size] = torch.from_numpy(np.ascontiguousarray(a))
+    return t
+
+
+def host(t: torch.Tensor) -> np.ndarray:
+    return t.cpu().numpy().view(np.uint16)
+
+
+# ---------------------------------------------------------------------------
+# Known answers and golden vectors.
+
+def test_kat_scalar_dropin(gpu):
+    kat = json.loads((GOLDEN / "kat.json").read_text())
+    for case in kat["ip_cksum"]:
+        if "hex_repeat" in case:
+            b, k = case["hex_repeat"]
+            data = bytes.fromhex(b) * k
+        else:
+            data = bytes.fromhex(case["hex"])
+        buf = data if data else b"\x00"
+        assert wc.ip_cksum(buf, len(data)) == int(case["expect"], 16), case["name"]
+
+
+def test_golden_vectors_ip(gpu):
+    g = np.load(GOLDEN / "vectors.npz")
+    out = wc.cksum_ragged(dev_u8(g["ip_blob"], gpu), to_dev(g["ip_off"], gpu),
+                          to_dev(g["ip_len"], gpu), kind="ip")
+    np.testing.assert_array_equal(host(out), g["ip_expect"])
+
+
+def test_golden_vectors_payload(gpu):
+    g = np.load(GOLDEN / "vectors.npz")
+    out = wc.cksum_ragged(dev_u8(g["pl_blob"], gpu), to_dev(g["pl_off"], gpu),
+                          to_dev(g["pl_len"], gpu), kind="payload")
+    np.testing.assert_array_equal(host(out), g["pl_expect"])
+
+
+# ---------------------------------------------------------------------------
+# Edge sweeps: lengths x start alignment x stride, both batch layouts.
+
+SWEEP_LENS = list(range(0, 131)) + [255, 256, 257, 511, 575, 576, 577, 1471, 1472,
+                                    1473, 2048, 4095, 8999, 9000, 9001, 65535]
+
+
+@pytest.mark.parametrize("length", SWEEP_LENS)
+def test_strided_sweep(gpu, length):
+    rng = np.random.default_rng(length)
+    n = 37
+    for stride in sorted({max(length, 1), (length + 15) // 16 * 16 or 16, length + 1}):
+        buf = rng.integers(0, 256, n * stride + 64, dtype=np.uint8)
+        d = dev_u8(buf, gpu)
+        for start in (0, 1, 2, 3, 7, 8, 14, 15):
+            if start + (n - 1) * stride + length > buf.size:
+                continue
+            got = host(wc.cksum_strided(d, stride, length, n, kind="ip", byte_offset=start))
+            want = c_oracle.cksum_strided(buf, stride, length, n, kind=0, byte_offset=start)
+            np.testing.assert_array_equal(got, want, err_msg=f"stride {stride} start {start}")
+
+
+def test_ragged_random_placement(gpu):
+    rng = np.random.default_rng(11)
+    buf = rng.integers(0, 256, 1 << 20, dtype=np.uint8)
+    n = 20000
+    lens = rng.integers(0, 9001, n).astype(np.uint16)
+    lens[:100] = 0
+    lens[100:200] = 1
+    offs = rng.integers(0, buf.size - 9001, n).astype(np.uint64)  # overlapping, unsorted
+    got = host(wc.cksum_ragged(dev_u8(buf, gpu), to_dev(offs, gpu), to_dev(lens, gpu)))
+    np.testing.assert_array_equal(got, c_oracle.cksum_ragged(buf, offs, lens, kind=0))
+
+
+def test_all_zero_and_all_ones(gpu):
+    for fill, want in ((0x00, 0xFFFF), (0xFF, 0x0000)):
+        buf = np.full(1472 * 64, fill, dtype=np.uint8)
+        got = host(wc.cksum_strided(dev_u8(buf, gpu), 1472, 1472, 64))
+        assert (got == want).all()
+
+
+def test_empty_batch_is_noop(gpu):
+    out = torch.full((4,), 7, dtype=torch.int16, device=gpu)
+    wc.cksum_strided(torch.zeros(16, dtype=torch.uint8, device=gpu), 16, 16, 0, out=out)
+    assert (out.cpu() == 7).all()
+
+
+# ---------------------------------------------------------------------------
+# payload_cksum (pseudo-header) batches.
+
+@pytest.mark.parametrize("align,lead", [(1, 0), (1, 3), (2, 14), (16, 14), (16, 0), (4, 1)])
+def test_payload_ragged_wild(gpu, align, lead):
+    rng = np.random.default_rng(100 + align * 17 + lead)
+    pkts = random_packets(rng, 3000, max_payload=1472, wild=True)
+    buf, offs, lens = pack(pkts, align=align, lead=lead)
+    got = host(wc.cksum_ragged(dev_u8(buf, gpu), to_dev(offs, gpu), to_dev(lens, gpu),
+                               kind="payload"))
+    np.testing.assert_array_equal(got, c_oracle.cksum_ragged(buf, offs, lens, kind=1))
+
+
+def test_payload_strided_netmap_layout(gpu):
+    """netmap-like slots: 2048-B buffers, IP header at base + 14 (eth.h:44-48)."""
+    rng = np.random.default_rng(7)
+    n, slot = 4096, 2048
+    buf = np.zeros(n * slot + 64, dtype=np.uint8)
+    for v6 in (False, True):
+        for i in range(n):
+            payload = rng.integers(0, 256, 1472 - (20 if v6 else 0), dtype=np.uint8).tobytes()
+            pkt, ln = (ipv6_udp if v6 else ipv4_udp)(payload, rng)
+            assert ln == 1500
+            buf[i * slot + 14: i * slot + 14 + len(pkt)] = np.frombuffer(pkt, np.uint8)
+        got = host(wc.cksum_strided(dev_u8(buf, gpu), slot, 1500, n, kind="payload",
+                                    byte_offset=14))
+        want = c_oracle.cksum_strided(buf, slot, 1500, n, kind=1, byte_offset=14)
+        np.testing.assert_array_equal(got, want)
+
+
+def test_payload_ipv6_wrap(gpu):
+    rng = np.random.default_rng(8)
+    pkts = [ipv6_udp(bytes([0xFF]) * p, rng, next_hdr=nh)
+            for p in (60000, 65000, 65487) for nh in (17, 58, 128, 200, 255)]
+    buf, offs, lens = pack(pkts, align=1, lead=5)
+    got = host(wc.cksum_ragged(dev_u8(buf, gpu), to_dev(offs, gpu), to_dev(lens, gpu),
+                               kind="payload"))
+    b = buf.tobytes()
+    want = [py_oracle.payload_cksum(b[o:o + n], n) for o, n in zip(offs, lens)]
+    np.testing.assert_array_equal(got, np.array(want, np.uint16))
+
+
+def test_verify_counts_bad_packets(gpu):
+    """RX verification (udp.c:132-139): packets carrying their checksum give 0."""
+    rng = np.random.default_rng(9)
+    pkts = random_packets(rng, 2000, max_payload=1400)
+    fixed, corrupt = [], 0
+    for k, (pkt, ln) in enumerate(pkts):
+        c = py_oracle.payload_cksum(pkt, ln)
+        if c == 0:       # the reference would send 0 = "no checksum" (udp.c:209-213)
+            continue
+        bad_one = k % 3 == 0
+        corrupt += bad_one
+        fixed.append((insert_checksum(pkt, c ^ 0x0101 if bad_one else c), ln))
+    buf, offs, lens = pack(fixed, align=2, lead=14)
+    out, bad = wc.verify_ragged(dev_u8(buf, gpu), to_dev(offs, gpu), to_dev(lens, gpu),
+                                kind="payload")
+    res = host(out)
+    assert int(bad.item()) == corrupt == int((res != 0).sum())
+    np.testing.assert_array_equal(res, c_oracle.cksum_ragged(buf, offs, lens, kind=1))
+
+
+def test_scalar_payload_dropin(gpu):
+    rng = np.random.default_rng(10)
+    for pkt, ln in random_packets(rng, 50, max_payload=1472, wild=True):
+        assert wc.payload_cksum(pkt, ln) == py_oracle.payload_cksum(pkt, ln)
+
+
+# ---------------------------------------------------------------------------
+# BASELINE.json configurations at full size (bit-exact over all packets).
+
+def synth_batch(gpu, nbytes, seed=synth.SEED):
+    d = torch.empty(nbytes + 64, dtype=torch.uint8, device=gpu)
+    wc.synth_fill(d, seed, nbytes=nbytes)
+    return d
+
+
+def test_c2_full_1m_x_1472(gpu):
+    n, L = 1 << 20, 1472
+    d = synth_batch(gpu, n * L)
+    got = host(wc.cksum_strided(d, L, L, n))
+    hb = d[: n * L].cpu().numpy()
+    np.testing.assert_array_equal(hb, c_oracle.synth(n * L, synth.SEED))
+    np.testing.assert_array_equal(got, c_oracle.cksum_strided(hb, L, L, n, kind=0))
+
+
+@pytest.mark.parametrize("L", [64, 256, 576, 1472, 9000])
+def test_c3_mtu_sweep_full(gpu, L):
+    n = 1 << 20
+    d = synth_batch(gpu, n * L, seed=synth.SEED ^ L)
+    got = host(wc.cksum_strided(d, L, L, n))
+    hb = d[: n * L].cpu().numpy()
+    np.testing.assert_array_equal(got, c_oracle.cksum_strided(hb, L, L, n, kind=0))
+
+
+def test_c4_zipf_full(gpu):
+    lens = synth.zipf_lengths(1 << 24)
+    offs = synth.packed_offsets(lens)
+    total = int(offs[-1]) + int(lens[-1])
+    d = synth_batch(gpu, total, seed=synth.ZIPF_SEED)
+    got = host(wc.cksum_ragged(d, to_dev(offs, gpu), to_dev(lens, gpu)))
+    hb = d[:total].cpu().numpy()
+    np.testing.assert_array_equal(got, c_oracle.cksum_ragged(hb, offs, lens, kind=0))
+
+
+def test_c2_roundtrip_property(gpu):
+    """Size-independent check: store each packet's checksum into its first
+    two bytes' place (zeroed), re-checksum -> every packet verifies to 0."""
+    n, L = 1 << 20, 1472
+    d = synth_batch(gpu, n * L, seed=42)
+    pk = d[: n * L].view(n, L)
+    pk[:, 0:2] = 0
+    c = wc.cksum_strided(d, L, L, n)
+    pk[:, 0:2] = c.view(torch.int16).view(torch.uint8).view(n, 2)
+    out, bad = wc.verify_strided(d, L, L, n, kind="ip")
+    assert int(bad.item()) == 0
+    assert (out.view(torch.int16) == 0).all()
+
+
+# ---------------------------------------------------------------------------
+# Host-memory (end-to-end) path and the C drop-in.
+
+@pytest.mark.parametrize("register", [False, True])
+def test_host_path(gpu, register):
+    rng = np.random.default_rng(12)
+    lens = synth.zipf_lengths(300000, seed=5)
+    offs = synth.packed_offsets(lens, lead=3)
+    buf = rng.integers(0, 256, int(offs[-1]) + int(lens[-1]) + 64, dtype=np.uint8)
+    if register:
+        wc.host_register(buf)
+    try:
+        got = wc.cksum_host(buf, offs, lens, kind="ip")
+    finally:
+        if register:
+            wc.host_unregister(buf)
+    np.testing.assert_array_equal(got, c_oracle.cksum_ragged(buf, offs, lens, kind=0))
+
+
+def test_c_dropin_program(gpu, tmp_path):
+    """A C caller linking libwccksum.so in place of in_cksum.c."""
+    exe = tmp_path / "dropin"
+    subprocess.run(["gcc", "-O2", "-std=gnu11", "-D__HIP_PLATFORM_AMD__",
+                    "-I/opt/rocm/include", f"-I{ROOT / 'include'}",
+                    str(ROOT / "tests" / "c" / "dropin_test.c"), "-o", str(exe),
+                    f"-L{ROOT / 'warpcore_amd'}", "-lwccksum", "-L/opt/rocm/lib",
+                    "-lamdhip64", f"-Wl,-rpath,{ROOT / 'warpcore_amd'}"], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "dropin: ok" in r.stdout

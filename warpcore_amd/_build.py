@@ -1,0 +1,99 @@
+"""Build recipes for the native pieces.
+
+* ``libwccksum.so`` -- the product: gfx950 HIP kernels + C ABI
+  (``include/warpcore_gpu/wc_cksum.h``), built in-tree with ``hipcc`` so the
+  ``.so`` travels with the repo snapshot to the GPU box.
+* ``oracle/libwc_oracle.so`` -- TEST INFRASTRUCTURE (parity checker / CPU
+  baseline).  Built per host CPU model (``-march=native``), into
+  ``oracle/build-<cpu>/`` so a box with a different host CPU rebuilds it.
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+import platform
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+PKG = ROOT / "warpcore_amd"
+CSRC = PKG / "csrc"
+INCLUDE = ROOT / "include"
+LIB = PKG / "libwccksum.so"
+ORACLE_DIR = ROOT / "oracle"
+
+HIP_SOURCES = [CSRC / "wc_cksum_kernels.hip", CSRC / "wc_cksum_api.cpp"]
+HIP_DEPS = HIP_SOURCES + [CSRC / "wc_cksum_kernels.h", INCLUDE / "warpcore_gpu" / "wc_cksum.h"]
+ORACLE_SOURCES = [ORACLE_DIR / "wc_oracle.c", ORACLE_DIR / "wc_oracle.h"]
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
+        if cand and (os.path.sep not in cand or os.path.exists(cand)):
+            return cand
+    return "hipcc"
+
+
+def _stale(target: Path, deps) -> bool:
+    if not target.exists():
+        return True
+    t = target.stat().st_mtime
+    return any(Path(d).stat().st_mtime > t for d in deps)
+
+
+def build_lib(force: bool = False, verbose: bool = False) -> Path:
+    """Compile libwccksum.so for gfx950 (cross-compiles without a GPU)."""
+    if not force and not _stale(LIB, HIP_DEPS):
+        return LIB
+    tmp = LIB.with_suffix(".so.tmp")
+    cmd = [
+        _hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
+        "-Wall", f"-I{INCLUDE}", f"-I{CSRC}", "-o", str(tmp),
+        *[str(s) for s in HIP_SOURCES],
+    ]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+def _cpu_tag() -> str:
+    model = platform.machine()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name") or line.startswith("flags"):
+                    model += line
+    except OSError:
+        pass
+    return hashlib.sha1(model.encode()).hexdigest()[:10]
+
+
+def oracle_path() -> Path:
+    return ORACLE_DIR / f"build-{_cpu_tag()}" / "libwc_oracle.so"
+
+
+def build_oracle(force: bool = False, verbose: bool = False) -> Path:
+    """Compile the CPU restatement (test infrastructure) for this host CPU."""
+    out = oracle_path()
+    if not force and not _stale(out, ORACLE_SOURCES):
+        return out
+    out.parent.mkdir(parents=True, exist_ok=True)
+    tmp = out.with_suffix(".so.tmp")
+    cmd = ["make", "-s", "-C", str(ORACLE_DIR), f"OUT={tmp}", "oracle"]
+    if verbose:
+        print(" ".join(cmd), file=sys.stderr)
+    subprocess.run(cmd, check=True)
+    os.replace(tmp, out)
+    return out
+
+
+def build_all(force: bool = False, verbose: bool = False) -> None:
+    build_lib(force=force, verbose=verbose)
+    build_oracle(force=force, verbose=verbose)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv, verbose=True)

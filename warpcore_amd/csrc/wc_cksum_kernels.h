@@ -1,0 +1,55 @@
+// wc_cksum_kernels.h -- internal interface between the C-ABI layer
+// (wc_cksum_api.cpp) and the gfx950 kernels (wc_cksum_kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define WC_KIND_IP 0
+#define WC_KIND_PAYLOAD 1
+
+// Every (group width, chunk loads per lane, packets per group-iteration)
+// shape the planner may pick; each is instantiated for both kinds, strided /
+// ragged, masked / unmasked and temporal / nontemporal loads.
+#define WC_SHAPE_LIST                                                          \
+    WC_SHAPE(4, 1, 4)                                                          \
+    WC_SHAPE(8, 1, 4)                                                          \
+    WC_SHAPE(16, 1, 4)                                                         \
+    WC_SHAPE(16, 2, 2)                                                         \
+    WC_SHAPE(16, 3, 2)                                                         \
+    WC_SHAPE(32, 2, 1)                                                         \
+    WC_SHAPE(32, 3, 1)                                                         \
+    WC_SHAPE(32, 4, 1)                                                         \
+    WC_SHAPE(64, 2, 1)                                                         \
+    WC_SHAPE(64, 4, 1)                                                         \
+    WC_SHAPE(64, 8, 1)
+
+namespace wc {
+
+struct LaunchArgs {
+    const void *base;
+    uint64_t stride;
+    uint32_t len;
+    const uint64_t *offs;
+    const uint16_t *lens;
+    uint64_t n;
+    uint16_t *out;
+    uint64_t *bad;
+    int kind;
+    bool ragged;
+    bool full;
+    bool nontemporal;
+};
+
+struct Shape {
+    int group;  // lanes per packet
+    int cpl;    // 16-byte chunk loads per lane per pass
+    int unroll; // packets per group per iteration
+};
+
+hipError_t launch_cksum(const LaunchArgs &a, const Shape &sh, int grid,
+                        hipStream_t st);
+hipError_t launch_synth(void *buf, uint64_t nbytes, uint64_t seed, int grid,
+                        hipStream_t st);
+
+} // namespace wc

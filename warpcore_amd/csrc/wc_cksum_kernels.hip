@@ -1,0 +1,378 @@
+// wc_cksum_kernels.hip -- gfx950 (MI355X / CDNA4) kernels for warpcore's
+// RFC 1071 Internet / UDP checksum.
+//
+// Reference semantics (read, not copied):
+//   /root/reference/lib/src/in_cksum.c:107-120  csum_oc16: Σ of native LE
+//       16-bit words into a uint32, odd trailing byte as a low byte;
+//   /root/reference/lib/src/in_cksum.c:74-80    csum_oc16_reduce: fold the
+//       end-around carry, complement;
+//   /root/reference/lib/src/in_cksum.c:133-137  ip_cksum;
+//   /root/reference/lib/src/in_cksum.c:140-167  payload_cksum (IPv4 / IPv6
+//       pseudo-header, header layouts ip4.h:55-66 and ip6.h:45-57).
+//
+// Design:
+//   * A packet is owned by a GROUP of G lanes of one wave64 (G = 64 is "one
+//     packet per wavefront"; smaller packets pack 64/G packets per wave).
+//   * The group streams the packet's 16-byte-aligned chunks with one
+//     global_load_dwordx4 per lane per chunk (coalesced; an aligned 16-byte
+//     chunk that overlaps the packet never crosses a page, so covering
+//     [start & ~15, end) can't fault even at an allocation's edge).
+//   * Each lane keeps two EXACT byte-lane sums with v_dot4_u32_u8: E = Σ bytes
+//     at even addresses, O = Σ bytes at odd addresses (masking and the IPv4 /
+//     IPv6 pseudo-header fields are folded into the dot4 byte weights).  The
+//     reference's uint32 accumulator is then exactly E + 256*O (packet starts
+//     at an even address) or O + 256*E (odd start), modulo 2^32 -- so results
+//     are bit-identical for every alignment, including the reference's uint32
+//     wrap-around on IPv6 next_hdr << 24 (in_cksum.c:157).
+//   * The group's partial sums are reduced with cross-lane adds, folded and
+//     complemented by the group leader, which stores the uint16.
+//   * No MFMA, no LDS tiles: this is a pure HBM-read stream (roofline: HBM).
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "wc_cksum_kernels.h"
+
+namespace wc {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// dot4 byte weights: bytes 0 and 2 of a dword sit at even addresses (the
+// chunk base is 16-byte aligned), bytes 1 and 3 at odd addresses.
+constexpr uint32_t kEvenW = 0x00010001u;
+constexpr uint32_t kOddW = 0x01000100u;
+
+__device__ __forceinline__ uint32_t dot4(uint32_t x, uint32_t w, uint32_t acc)
+{
+    return __builtin_amdgcn_udot4(x, w, acc, false);
+}
+
+// Byte mask (0xFF per selected byte) of the bytes of dword j (bytes 4j..4j+3
+// of a 16-byte chunk) that fall in [lo, hi), both relative to the chunk.
+__device__ __forceinline__ uint32_t dword_mask(int lo, int hi, int j)
+{
+    const int l = min(max(lo - 4 * j, 0), 4);
+    const int h = min(max(hi - 4 * j, 0), 4);
+    const uint64_t m = ((1ull << (8 * h)) - 1ull) & ~((1ull << (8 * l)) - 1ull);
+    return (uint32_t)m;
+}
+
+__device__ __forceinline__ uint32_t pick_dword(const u32x4 &d, int j)
+{
+    return j == 0 ? d.x : j == 1 ? d.y : j == 2 ? d.z : d.w;
+}
+
+__device__ __forceinline__ uint32_t pick_byte(const u32x4 &d, int pos)
+{
+    return (pick_dword(d, pos >> 2) >> (8 * (pos & 3))) & 0xFFu;
+}
+
+// Global (addrspace 1) pointer: lets hipcc emit global_load_dwordx4 rather
+// than flat loads for addresses computed as integers.
+typedef const u32x4 __attribute__((address_space(1))) *gchunk_ptr;
+
+template <bool NT>
+__device__ __forceinline__ u32x4 load_chunk(uint64_t addr)
+{
+    gchunk_ptr p = (gchunk_ptr)(uintptr_t)addr;
+    if constexpr (NT)
+        return __builtin_nontemporal_load(p);
+    else
+        return *p;
+}
+
+// in_cksum.c:74-80 -- two end-around folds always suffice for a uint32.
+__device__ __forceinline__ uint16_t fold_not(uint32_t s)
+{
+    s = (s & 0xFFFFu) + (s >> 16);
+    s = (s & 0xFFFFu) + (s >> 16);
+    return (uint16_t)~s;
+}
+
+template <int G>
+__device__ __forceinline__ uint32_t group_sum(uint32_t v)
+{
+#pragma unroll
+    for (int m = G / 2; m >= 1; m >>= 1)
+        v += __shfl_xor(v, m, 64);
+    return v;
+}
+
+// Accumulate one 16-byte chunk.  `co` = chunk start minus packet start (may be
+// negative for the first chunk of an unaligned packet); bytes whose packet
+// offset lies in [rs, re) get weight 1, and for payload_cksum the pseudo-header
+// fields that the reference adds with natural word weighting get one more.
+template <int KIND, bool FULL>
+__device__ __forceinline__ void accum_chunk(const u32x4 &d, int co, int rs,
+                                            int re, bool v4, uint32_t &E,
+                                            uint32_t &O)
+{
+    if constexpr (FULL) {
+        E = dot4(d.x, kEvenW, E);
+        O = dot4(d.x, kOddW, O);
+        E = dot4(d.y, kEvenW, E);
+        O = dot4(d.y, kOddW, O);
+        E = dot4(d.z, kEvenW, E);
+        O = dot4(d.z, kOddW, O);
+        E = dot4(d.w, kEvenW, E);
+        O = dot4(d.w, kOddW, O);
+    } else {
+        const int lo = rs - co, hi = re - co;
+        const bool hdr = KIND == WC_KIND_PAYLOAD && co < 40;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t m = dword_mask(lo, hi, j);
+            uint32_t we = kEvenW & m, wo = kOddW & m;
+            if (KIND == WC_KIND_PAYLOAD && hdr) {
+                // IPv4: proto @9 (reference adds p << 8, the natural weight of
+                // an odd byte), src/dst @12..19 (in_cksum.c:149-151).
+                // IPv6: payload length @4..5, src/dst @8..39
+                // (in_cksum.c:158-160).  Intervals within one version are
+                // disjoint, so OR-ing their masks is exact; adding to the
+                // range weight reproduces the reference's double count when a
+                // malformed IHL (< 5) makes the payload overlap src/dst.
+                const uint32_t h =
+                    v4 ? (dword_mask(9 - co, 10 - co, j) |
+                          dword_mask(12 - co, 20 - co, j))
+                       : (dword_mask(4 - co, 6 - co, j) |
+                          dword_mask(8 - co, 40 - co, j));
+                we += kEvenW & h;
+                wo += kOddW & h;
+            }
+            const uint32_t x = pick_dword(d, j);
+            E = dot4(x, we, E);
+            O = dot4(x, wo, O);
+        }
+    }
+}
+
+// Packet batch kernel.
+//   G     lanes per packet (power of two, 4..64)
+//   CPL   16-byte chunk loads per lane per pass (a pass covers G*CPL chunks)
+//   U     packets per group per iteration (more bytes in flight for small
+//         packets)
+//   KIND  WC_KIND_IP / WC_KIND_PAYLOAD
+//   RAGGED offsets/lengths from device arrays instead of i*stride / len
+//   FULL  every packet starts 16-byte aligned and len % 16 == 0 (IP only):
+//         no masks
+//   NT    nontemporal loads
+template <int G, int CPL, int U, int KIND, bool RAGGED, bool FULL, bool NT>
+__global__ void __launch_bounds__(256)
+k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len_fixed,
+        const uint64_t *__restrict__ offs, const uint16_t *__restrict__ lens,
+        uint64_t n, uint16_t *__restrict__ out,
+        unsigned long long *__restrict__ bad)
+{
+    static_assert(G >= 4 && G <= 64 && (G & (G - 1)) == 0, "group width");
+    constexpr int GPW = 64 / G;
+    constexpr uint64_t PPW = (uint64_t)GPW * U;
+    constexpr int PASS = G * CPL;
+
+    const int lane = threadIdx.x & 63;
+    const int gl = lane & (G - 1);
+    const int grp = lane / G;
+    const int lead = lane & ~(G - 1);
+    const uint64_t wave =
+        (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    uint32_t nbad = 0;
+
+    for (uint64_t p0 = wave * PPW; p0 < n; p0 += nwaves * PPW) {
+        uint64_t c0[U];
+        uint32_t nch[U], plen[U];
+        int s[U];
+        bool valid[U];
+        u32x4 d[U][CPL];
+
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = p0 + (uint64_t)u * GPW + grp;
+            valid[u] = i < n;
+            const uint64_t ii = valid[u] ? i : p0;
+            const uint64_t off = RAGGED ? offs[ii] : ii * stride;
+            const uint32_t l = RAGGED ? (uint32_t)lens[ii] : len_fixed;
+            const uint64_t a = (uint64_t)base + off;
+            // payload_cksum reads the IPv4 header fields up to byte 19 even
+            // for a shorter len (in_cksum.c:149-151), so cover them too.
+            const uint32_t span = KIND == WC_KIND_PAYLOAD ? max(l, 20u) : l;
+            plen[u] = l;
+            s[u] = (int)(a & 15u);
+            c0[u] = a & ~15ull;
+            nch[u] = valid[u] ? (uint32_t)((a + span + 15u - c0[u]) >> 4) : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const uint32_t k = (uint32_t)(gl + c * G);
+                d[u][c] = k < nch[u] ? load_chunk<NT>(c0[u] + 16ull * k)
+                                     : u32x4{0u, 0u, 0u, 0u};
+            }
+        }
+
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            int rs = 0;
+            bool v4 = true;
+            uint32_t special = 0;
+            if constexpr (KIND == WC_KIND_PAYLOAD) {
+                // Bytes 0, 2, 3, 6 of the header sit in the group's chunks 0/1,
+                // i.e. in d[u][0] of group lanes 0 and 1.
+                const int su = s[u];
+                const uint32_t b0 =
+                    __shfl(pick_byte(d[u][0], su & 15), lead + (su >> 4), 64);
+                const uint32_t b2 = __shfl(pick_byte(d[u][0], (su + 2) & 15),
+                                           lead + ((su + 2) >> 4), 64);
+                const uint32_t b3 = __shfl(pick_byte(d[u][0], (su + 3) & 15),
+                                           lead + ((su + 3) >> 4), 64);
+                const uint32_t b6 = __shfl(pick_byte(d[u][0], (su + 6) & 15),
+                                           lead + ((su + 6) >> 4), 64);
+                v4 = (b0 >> 4) == 4u;                        // ip4.h:75-79
+                const uint32_t hl = v4 ? (b0 & 15u) * 4u : 40u; // ip4.h:88-92
+                rs = (int)hl;
+                if (gl == 0) {
+                    if (v4) {
+                        // plen = bswap16(bswap16(ip->len) - hl) read as a
+                        // native word (in_cksum.c:152-153).
+                        const uint32_t x = (((b2 << 8) | b3) - hl) & 0xFFFFu;
+                        special = ((x & 0xFFu) << 8) | (x >> 8);
+                    } else {
+                        special = b6 << 24;                 // in_cksum.c:157
+                    }
+                }
+            }
+            const int re = (int)plen[u];
+
+            uint32_t E = 0, O = 0;
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const int co = 16 * (gl + c * G) - s[u];
+                accum_chunk<KIND, FULL>(d[u][c], co, rs, re, v4, E, O);
+            }
+            // Packets longer than one pass (e.g. 9000 B jumbo frames).
+            for (uint32_t kb = PASS; kb < nch[u]; kb += PASS) {
+                u32x4 t[CPL];
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) {
+                    const uint32_t k = kb + (uint32_t)(gl + c * G);
+                    t[c] = k < nch[u] ? load_chunk<NT>(c0[u] + 16ull * k)
+                                      : u32x4{0u, 0u, 0u, 0u};
+                }
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) {
+                    const int co = 16 * (int)(kb + gl + c * G) - s[u];
+                    accum_chunk<KIND, FULL>(t[c], co, rs, re, v4, E, O);
+                }
+            }
+
+            // Exact reference accumulator, modulo 2^32 like its uint32.
+            uint32_t S = (s[u] & 1) ? O + (E << 8) : E + (O << 8);
+            S += special;
+            S = group_sum<G>(S);
+            if (gl == 0 && valid[u]) {
+                const uint16_t r = fold_not(S);
+                const uint64_t i = p0 + (uint64_t)u * GPW + grp;
+                if (out)
+                    out[i] = r;
+                nbad += r != 0;
+            }
+        }
+    }
+
+    if (bad) {
+        // Wave-level total of the leaders' counts, one atomic per wave.
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1)
+            nbad += __shfl_xor(nbad, m, 64);
+        if (lane == 0 && nbad)
+            atomicAdd(bad, (unsigned long long)nbad);
+    }
+}
+
+// splitmix64 output k for state `seed` (must match oracle_synth_fill).
+__device__ __forceinline__ uint64_t splitmix64_at(uint64_t seed, uint64_t k)
+{
+    uint64_t z = seed + (k + 1ull) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ void __launch_bounds__(256)
+k_synth(uint8_t *__restrict__ buf, uint64_t nbytes, uint64_t seed)
+{
+    const uint64_t words = nbytes / 8;
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
+    // Two words (16 B) per thread per step; buf is 16-byte aligned by contract.
+    for (uint64_t w = 2 * tid; w < words; w += 2 * nth) {
+        if (w + 1 < words) {
+            uint64_t v[2] = {splitmix64_at(seed, w), splitmix64_at(seed, w + 1)};
+            *reinterpret_cast<u32x4 *>(buf + 8 * w) =
+                *reinterpret_cast<const u32x4 *>(v);
+        } else {
+            *reinterpret_cast<uint64_t *>(buf + 8 * w) = splitmix64_at(seed, w);
+        }
+    }
+    if (tid == 0 && (nbytes & 7u)) {
+        const uint64_t v = splitmix64_at(seed, words);
+        for (uint32_t b = 0; b < (nbytes & 7u); ++b)
+            buf[8 * words + b] = (uint8_t)(v >> (8 * b));
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Launch table.
+
+template <int G, int CPL, int U, int KIND, bool RAGGED, bool FULL, bool NT>
+static hipError_t launch_one(const LaunchArgs &a, int grid, hipStream_t st)
+{
+    hipLaunchKernelGGL((k_cksum<G, CPL, U, KIND, RAGGED, FULL, NT>), dim3(grid),
+                       dim3(256), 0, st, (const uint8_t *)a.base, a.stride,
+                       a.len, a.offs, a.lens, a.n, a.out,
+                       (unsigned long long *)a.bad);
+    return hipGetLastError();
+}
+
+template <int G, int CPL, int U>
+static hipError_t launch_shape(const LaunchArgs &a, int grid, hipStream_t st)
+{
+    const bool nt = a.nontemporal;
+    if (a.kind == WC_KIND_PAYLOAD) {
+        if (a.ragged)
+            return nt ? launch_one<G, CPL, U, WC_KIND_PAYLOAD, true, false, true>(a, grid, st)
+                      : launch_one<G, CPL, U, WC_KIND_PAYLOAD, true, false, false>(a, grid, st);
+        return nt ? launch_one<G, CPL, U, WC_KIND_PAYLOAD, false, false, true>(a, grid, st)
+                  : launch_one<G, CPL, U, WC_KIND_PAYLOAD, false, false, false>(a, grid, st);
+    }
+    if (a.ragged)
+        return nt ? launch_one<G, CPL, U, WC_KIND_IP, true, false, true>(a, grid, st)
+                  : launch_one<G, CPL, U, WC_KIND_IP, true, false, false>(a, grid, st);
+    if (a.full)
+        return nt ? launch_one<G, CPL, U, WC_KIND_IP, false, true, true>(a, grid, st)
+                  : launch_one<G, CPL, U, WC_KIND_IP, false, true, false>(a, grid, st);
+    return nt ? launch_one<G, CPL, U, WC_KIND_IP, false, false, true>(a, grid, st)
+              : launch_one<G, CPL, U, WC_KIND_IP, false, false, false>(a, grid, st);
+}
+
+// The shapes the planner may choose (wc_cksum_plan.cpp keeps the same list).
+hipError_t launch_cksum(const LaunchArgs &a, const Shape &sh, int grid,
+                        hipStream_t st)
+{
+#define WC_SHAPE(G_, C_, U_)                                                   \
+    if (sh.group == G_ && sh.cpl == C_ && sh.unroll == U_)                     \
+        return launch_shape<G_, C_, U_>(a, grid, st);
+    WC_SHAPE_LIST
+#undef WC_SHAPE
+    return hipErrorInvalidValue;
+}
+
+hipError_t launch_synth(void *buf, uint64_t nbytes, uint64_t seed, int grid,
+                        hipStream_t st)
+{
+    hipLaunchKernelGGL(k_synth, dim3(grid), dim3(256), 0, st, (uint8_t *)buf,
+                       nbytes, seed);
+    return hipGetLastError();
+}
+
+} // namespace wc
