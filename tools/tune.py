@@ -1,0 +1,157 @@
+#!/usr/bin/env python3
+"""Interleaved A/B timing of kernel variants in ONE process (guide rule 24).
+
+    python tools/tune.py [--config c2|c3|c4] [--len L] [--rounds R] [--iters I]
+                         [--variants spec;spec;...] [--ceiling]
+
+A variant spec is a comma-free env string, e.g.
+"WC_SHAPE=32,3,1 WC_NT=1 WC_BLOCKS_PER_CU=4".  Each round runs every variant
+for I launches timed with HIP events on the launch stream; the table reports
+median and best GB/s (payload bytes / kernel time) per variant.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import os
+import statistics
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import warpcore_amd as wc  # noqa: E402
+from warpcore_amd import synth  # noqa: E402
+
+
+def stream_lib():
+    so = ROOT / "tools" / "libstream_ceiling.so"
+    src = ROOT / "tools" / "stream_ceiling.hip"
+    if not so.exists() or so.stat().st_mtime < src.stat().st_mtime:
+        subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-fPIC",
+                        "-shared", "-o", str(so), str(src)], check=True)
+    lib = ctypes.CDLL(str(so))
+    lib.stream_read.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
+                                ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    return lib
+
+
+def time_it(fn, iters, stream):
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(iters):
+        fn()
+    e1.record(stream)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / iters  # ms
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--len", type=int, default=1472)
+    ap.add_argument("--packets", type=int, default=1 << 20)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--variants", default="")
+    ap.add_argument("--ceiling", action="store_true")
+    ap.add_argument("--json", default="")
+    ap.add_argument("--ragged", action="store_true",
+                    help="c2/c3 through the ragged entry point (offset/length arrays)")
+    args = ap.parse_args()
+
+    dev = torch.device("cuda:0")
+    wc.gpu_init(0)
+    stream = torch.cuda.current_stream()
+    if args.config == "c4":
+        n = args.packets if args.packets != (1 << 20) else 1 << 24
+        lens = synth.zipf_lengths(n)
+        offs = synth.packed_offsets(lens)
+        nbytes = int(lens.astype(np.uint64).sum())
+        buf = torch.empty(nbytes + 64, dtype=torch.uint8, device=dev)
+        wc.synth_fill(buf, 1, nbytes=nbytes)
+        d_off, d_len = torch.from_numpy(offs).to(dev), torch.from_numpy(lens).to(dev)
+        out = torch.empty(n, dtype=torch.uint16, device=dev)
+        run = lambda: wc.cksum_ragged(buf, d_off, d_len, out=out)  # noqa: E731
+    else:
+        L = 1472 if args.config == "c2" else args.len
+        n = args.packets
+        nbytes = n * L
+        buf = torch.empty(nbytes + 64, dtype=torch.uint8, device=dev)
+        wc.synth_fill(buf, 1, nbytes=nbytes)
+        out = torch.empty(n, dtype=torch.uint16, device=dev)
+        run = lambda: wc.cksum_strided(buf, L, L, n, out=out)  # noqa: E731
+        if args.ragged:
+            d_off = torch.arange(n, dtype=torch.int64, device=dev) * L
+            d_len = torch.full((n,), L, dtype=torch.int16, device=dev)
+            run = lambda: wc.cksum_ragged(buf, d_off, d_len, out=out)  # noqa: E731
+
+    variants = [v.strip() for v in args.variants.split(";") if v.strip()] or [""]
+    base_env = {k: os.environ.get(k) for k in ("WC_SHAPE", "WC_NT", "WC_BLOCKS_PER_CU", "WC_GRID",
+                                                "WC_FLAT_UN", "WC_RAGGED", "WC_FLAT_TPW")}
+
+    def apply(spec):
+        for k, v in base_env.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+        for kv in spec.split():
+            k, v = kv.split("=", 1)
+            os.environ[k] = v
+
+    cases = [(v, None) for v in variants]
+    slib = None
+    if args.ceiling:
+        slib = stream_lib()
+        sink = torch.zeros(1 << 22, dtype=torch.int32, device=dev)
+        for grid in (1024, 2048, 4096, 8192):
+            for unroll in (2, 4, 8):
+                for nt in (0, 1):
+                    cases.append((f"READ grid={grid} unroll={unroll} nt={nt}", (grid, unroll, nt)))
+
+    times = {c[0]: [] for c in cases}
+    ref = None
+    for r in range(args.rounds):
+        for name, cfg in cases:
+            if cfg is None:
+                apply(name)
+                run()  # warm + plan
+                ms = time_it(run, args.iters, stream)
+                if r == 0:
+                    res = out.cpu().numpy().view(np.uint16).copy()
+                    if ref is None:
+                        ref = res
+                    elif not np.array_equal(ref, res):
+                        print(f"!! variant {name!r} results differ", flush=True)
+            else:
+                g, u, nt = cfg
+                fn = lambda: slib.stream_read(buf.data_ptr(), nbytes, g, u, nt,  # noqa: E731
+                                              sink.data_ptr(), stream.cuda_stream)
+                fn()
+                ms = time_it(fn, args.iters, stream)
+            times[name].append(ms)
+    apply("")
+    rows = []
+    for name, ts in times.items():
+        med, best = statistics.median(ts), min(ts)
+        rows.append({"variant": name or "default", "ms_med": med, "ms_best": best,
+                     "GBps_med": nbytes / med / 1e6, "GBps_best": nbytes / best / 1e6})
+    for row in rows:
+        print(f"{row['variant']:<48} {row['ms_med']*1e3:9.1f} us  "
+              f"{row['GBps_med']:8.1f} GB/s med  {row['GBps_best']:8.1f} best  "
+              f"{row['GBps_med']/8000*100:5.1f}% of 8 TB/s", flush=True)
+    if args.json:
+        Path(args.json).write_text(json.dumps({"config": args.config, "bytes": nbytes,
+                                               "rows": rows}, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -139,28 +139,28 @@ int ensure_device(Device **out)
 
 wc::Shape shape_for_chunks(uint32_t nch)
 {
-    // Smallest group that covers the packet in one pass with few loads per
-    // lane; small packets get U > 1 so every lane keeps >= 2-4 loads in
-    // flight.
+    // Smallest group covering the packet in one pass, with U packets per
+    // group so every lane keeps ~4-18 16-byte loads in flight (tuned on
+    // MI355X: DESIGN.md section 5, profiles/tune_r01_*.log).
     if (nch <= 4)
-        return {4, 1, 4};
+        return {4, 1, 8};
     if (nch <= 8)
         return {8, 1, 4};
     if (nch <= 16)
         return {16, 1, 4};
     if (nch <= 32)
-        return {16, 2, 2};
+        return {16, 2, 4};
     if (nch <= 48)
-        return {16, 3, 2};
-    if (nch <= 64)
-        return {32, 2, 1};
+        return {16, 3, 4};
     if (nch <= 96)
-        return {32, 3, 1};
+        return {16, 6, 4};
     if (nch <= 128)
         return {32, 4, 1};
     if (nch <= 256)
         return {64, 4, 1};
-    return {64, 8, 1};
+    if (nch <= 576)
+        return {32, 18, 1};
+    return {64, 9, 1};
 }
 
 bool shape_override(wc::Shape *sh)
@@ -182,8 +182,14 @@ int grid_for(const Device &D, const wc::Shape &sh, uint64_t n)
     const uint64_t ppw = (uint64_t)(64 / sh.group) * sh.unroll;
     const uint64_t waves = (n + ppw - 1) / ppw;
     const uint64_t blocks = (waves + 3) / 4;
-    const int per_cu = env_int("WC_BLOCKS_PER_CU", 8);
-    uint64_t cap = (uint64_t)D.cus * (uint64_t)std::max(per_cu, 1);
+    // One-shot grid by default: every block handles one wave-iteration per
+    // wave and retires (measured faster than a resident grid-stride loop on
+    // MI355X: DESIGN.md section 5).  WC_BLOCKS_PER_CU / WC_GRID cap it into a
+    // grid-stride launch for experiments.
+    uint64_t cap = 0x7FFFFFFFull;
+    const int per_cu = env_int("WC_BLOCKS_PER_CU", 0);
+    if (per_cu > 0)
+        cap = (uint64_t)D.cus * (uint64_t)per_cu;
     const int fixed = env_int("WC_GRID", 0);
     if (fixed > 0)
         cap = (uint64_t)fixed;
@@ -215,21 +221,28 @@ Plan plan_strided(const Device &D, uint64_t base, uint64_t stride, uint32_t len,
 Plan plan_ragged(const Device &D, uint64_t n)
 {
     Plan p;
-    // Lengths live on the device; size the group for typical MTU-bounded
-    // traffic (longer packets take more passes inside the kernel).
-    p.shape = {16, 2, 2};
-    shape_override(&p.shape);
+    // Default: the chunk-balanced flat kernel (group = 0 marks it; unroll =
+    // 64-chunk rows in flight per lane).  WC_RAGGED=group selects the
+    // group-per-packet kernel (shape from WC_SHAPE) for comparison.
+    p.shape = {0, 1, env_int("WC_FLAT_UN", 1)};
+    const char *mode = getenv("WC_RAGGED");
+    if (mode && !strcmp(mode, "group")) {
+        p.shape = {16, 2, 2};
+        shape_override(&p.shape);
+    }
     p.full = false;
-    p.grid = grid_for(D, p.shape, n);
+    p.grid = p.shape.group ? grid_for(D, p.shape, n) : 0;
     return p;
 }
 
-bool nontemporal() { return env_int("WC_NT", 0) != 0; }
+bool nontemporal() { return env_int("WC_NT", 1) != 0; }
+int flat_tpw() { return env_int("WC_FLAT_TPW", 1); }
 
 int run(const Device &D, const wc::LaunchArgs &a, const Plan &p, hipStream_t st)
 {
     (void)D;
-    hipError_t e = wc::launch_cksum(a, p.shape, p.grid, st);
+    hipError_t e = p.shape.group == 0 ? wc::launch_flat(a, p.shape.unroll, st)
+                                      : wc::launch_cksum(a, p.shape, p.grid, st);
     return hip_err(e);
 }
 
@@ -268,7 +281,7 @@ int batch_ragged(const void *d_base, const uint64_t *d_off, const uint16_t *d_le
         return rc;
     const Plan p = plan_ragged(*D, n);
     wc::LaunchArgs a{d_base, 0,     0,    d_off, d_len, n,
-                     d_out,  d_bad, kind, true,  false, nontemporal()};
+                     d_out,  d_bad, kind, true,  false, nontemporal(), flat_tpw()};
     return run(*D, a, p, (hipStream_t)stream);
 }
 
@@ -506,7 +519,7 @@ int wc_cksum_host(const void *h_base, uint64_t h_bytes, const uint64_t *h_off,
         const Plan p = plan_ragged(*D, cnt);
         wc::LaunchArgs a{P.d_bytes[slot], 0,    0,    P.d_off[slot], P.d_len[slot],
                          cnt,             P.d_out[slot], nullptr, kind, true,
-                         false,           nontemporal()};
+                         false,           nontemporal(), flat_tpw()};
         rc = run(*D, a, p, st);
         if (rc)
             return rc;

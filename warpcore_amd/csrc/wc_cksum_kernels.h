@@ -13,16 +13,33 @@
 // ragged, masked / unmasked and temporal / nontemporal loads.
 #define WC_SHAPE_LIST                                                          \
     WC_SHAPE(4, 1, 4)                                                          \
+    WC_SHAPE(4, 1, 8)                                                          \
+    WC_SHAPE(4, 1, 16)                                                         \
     WC_SHAPE(8, 1, 4)                                                          \
+    WC_SHAPE(8, 1, 8)                                                          \
+    WC_SHAPE(8, 2, 4)                                                          \
     WC_SHAPE(16, 1, 4)                                                         \
+    WC_SHAPE(16, 1, 8)                                                         \
     WC_SHAPE(16, 2, 2)                                                         \
+    WC_SHAPE(16, 2, 4)                                                         \
     WC_SHAPE(16, 3, 2)                                                         \
+    WC_SHAPE(16, 3, 4)                                                         \
+    WC_SHAPE(16, 4, 2)                                                         \
+    WC_SHAPE(16, 6, 1)                                                         \
+    WC_SHAPE(16, 6, 2)                                                         \
+    WC_SHAPE(16, 6, 4)                                                         \
     WC_SHAPE(32, 2, 1)                                                         \
     WC_SHAPE(32, 3, 1)                                                         \
+    WC_SHAPE(32, 3, 2)                                                         \
+    WC_SHAPE(32, 3, 4)                                                         \
+    WC_SHAPE(32, 3, 8)                                                         \
     WC_SHAPE(32, 4, 1)                                                         \
+    WC_SHAPE(32, 18, 1)                                                        \
     WC_SHAPE(64, 2, 1)                                                         \
     WC_SHAPE(64, 4, 1)                                                         \
-    WC_SHAPE(64, 8, 1)
+    WC_SHAPE(64, 8, 1)                                                         \
+    WC_SHAPE(64, 9, 1)                                                         \
+    WC_SHAPE(64, 9, 2)
 
 namespace wc {
 
@@ -39,6 +56,7 @@ struct LaunchArgs {
     bool ragged;
     bool full;
     bool nontemporal;
+    int tiles_per_wave; // flat kernel: 64-packet tiles each wave walks
 };
 
 struct Shape {
@@ -49,6 +67,9 @@ struct Shape {
 
 hipError_t launch_cksum(const LaunchArgs &a, const Shape &sh, int grid,
                         hipStream_t st);
+// Chunk-balanced kernel for ragged batches (unroll = 64-chunk rows per lane
+// in flight: 1, 2, 4 or 8).
+hipError_t launch_flat(const LaunchArgs &a, int unroll, hipStream_t st);
 hipError_t launch_synth(void *buf, uint64_t nbytes, uint64_t seed, int grid,
                         hipStream_t st);
 

@@ -31,6 +31,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "wc_cksum_kernels.h"
 
 namespace wc {
@@ -289,6 +291,311 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len_fixed,
     }
 }
 
+// ---------------------------------------------------------------------------
+// Ragged batches: chunk-balanced "flat" kernel.
+//
+// A wave owns a tile of 64 consecutive packets (lane l holds packet l's
+// metadata, loaded coalesced).  The tile's 16-byte chunks are numbered
+// 0..T-1 in packet order (wave prefix sum of the per-packet chunk counts) and
+// dealt to the lanes one 64-chunk ROW at a time, so every lane streams a chunk
+// whatever the length mix (Zipf, jumbo frames, empty packets).  Per row:
+//   * owner lookup: each packet whose run of chunks starts inside the row
+//     marks that slot in LDS (tagged with the row number, so nothing needs
+//     clearing); a ballot of the marks gives the run starts, and
+//     rank(owner) = rank(first run) + mbcnt(starts at or below the lane);
+//   * the owner's descriptor (chunk base, start phase, length, header info)
+//     is one ds_read_b128 from the tile's LDS table, indexed by the rank of
+//     the packet among the tile's non-empty packets;
+//   * byte masks come from a 17 x 17 LDS table (bytes [lo, hi) of a chunk);
+//   * the lanes' exact partial sums go through a DPP inclusive prefix sum and
+//     each packet lane adds P[last slot] - P[first slot - 1] of its run to a
+//     register accumulator -- no atomics, no same-address LDS traffic.
+// Row groups of UN rows are double-buffered and the next tile's metadata is
+// prefetched while the current tile streams.
+constexpr int kFlatWaves = 4; // 256-thread blocks
+
+// DPP controls (GFX9 family, gfx950 included).
+constexpr int kDppRowShr = 0x110; // + 1..15
+constexpr int kDppRowBcast15 = 0x142;
+constexpr int kDppRowBcast31 = 0x143;
+
+// Lanes whose DPP source is outside the row / disabled read 0.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp0(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWS, 0xF, true);
+}
+
+// Inclusive wave64 prefix sum (mod 2^32).
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v)
+{
+    v += dpp0<kDppRowShr + 1, 0xF>(v);
+    v += dpp0<kDppRowShr + 2, 0xF>(v);
+    v += dpp0<kDppRowShr + 4, 0xF>(v);
+    v += dpp0<kDppRowShr + 8, 0xF>(v);
+    v += dpp0<kDppRowBcast15, 0xA>(v); // rows 1, 3 += end of rows 0, 2
+    v += dpp0<kDppRowBcast31, 0xC>(v); // rows 2, 3 += end of row 1
+    return v;
+}
+
+struct FlatDesc {          // 16 bytes per non-empty packet of the tile, in LDS
+    uint32_t vb_lo, vb_hi; // chunk q of the packet sits at vb + 16 q
+    uint32_t rel;          // packet start in the tile's slot-byte space
+    uint32_t info;         // len | hl << 16 | v4 << 24
+};
+
+template <int UN>
+struct FlatRows {
+    u32x4 d[UN];
+    uint32_t rel[UN], info[UN];
+};
+
+template <int UN>
+struct FlatLds {
+    FlatDesc desc[64];
+    uint32_t mark[2 * UN][64];
+};
+
+// keep[lo * 17 + hi] = 0x01 in every byte b of a chunk with lo <= b < hi.
+struct FlatMaskLut {
+    u32x4 keep[17 * 17];
+};
+
+__device__ __forceinline__ void build_mask_lut(FlatMaskLut &M)
+{
+    for (int i = threadIdx.x; i < 17 * 17; i += blockDim.x) {
+        const int lo = i / 17, hi = i % 17;
+        uint32_t w[4];
+        for (int j = 0; j < 4; ++j) {
+            uint32_t v = 0;
+            for (int b = 0; b < 4; ++b) {
+                const int pos = 4 * j + b;
+                v |= (pos >= lo && pos < hi ? 1u : 0u) << (8 * b);
+            }
+            w[j] = v;
+        }
+        M.keep[i] = u32x4{w[0], w[1], w[2], w[3]};
+    }
+}
+
+__device__ __forceinline__ void wave_sync_lds()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int UN, bool NT>
+__device__ __forceinline__ void flat_issue(FlatRows<UN> &R, FlatLds<UN> &L,
+                                           uint32_t j, int lane, uint32_t cp,
+                                           uint32_t ce, uint32_t rank,
+                                           uint32_t total)
+{
+#pragma unroll
+    for (int u = 0; u < UN; ++u) {
+        const uint32_t row0 = j + 64u * u;
+        const uint32_t tag = row0 >> 6;
+        uint32_t *mark = L.mark[tag % (2 * UN)];
+        // Packet lane: its run inside this row is [lo, hi).
+        const uint32_t lo = max(cp, row0), hi = min(ce, row0 + 64u);
+        const bool part = lo < hi;
+        if (part && lo > row0)
+            mark[lo - row0] = tag;
+        // Rank of the packet covering the row's first slot.
+        const uint64_t firstm = __ballot(part && lo == row0);
+        const int fl = firstm ? (int)__builtin_ctzll(firstm) : 0;
+        const uint32_t first = __builtin_amdgcn_readlane(rank, fl);
+        wave_sync_lds();
+        const bool start = mark[lane] == tag;
+        const uint64_t starts = __ballot(start);
+        const uint32_t below = __builtin_amdgcn_mbcnt_hi(
+            (uint32_t)(starts >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)starts, 0u));
+        const uint32_t owner = min(first + below + (start ? 1u : 0u), 63u);
+        const FlatDesc g = L.desc[owner];
+        R.rel[u] = g.rel;
+        R.info[u] = g.info;
+        // Unconditional load (slots past the tile's end re-read its last
+        // chunk and are zeroed in flat_accum) keeps the issue stream
+        // straight-line, so hipcc can wait for exactly the older row group.
+        const uint32_t q = min(row0 + (uint32_t)lane, total - 1u);
+        const uint64_t vb = ((uint64_t)g.vb_hi << 32) | g.vb_lo;
+        R.d[u] = load_chunk<NT>(vb + 16ull * q);
+    }
+}
+
+template <int UN, int KIND>
+__device__ __forceinline__ void flat_accum(const FlatRows<UN> &R,
+                                           const FlatMaskLut &M, uint32_t j,
+                                           int lane, uint32_t cp, uint32_t ce,
+                                           uint32_t total, uint32_t &acc)
+{
+#pragma unroll
+    for (int u = 0; u < UN; ++u) {
+        const uint32_t row0 = j + 64u * u;
+        const uint32_t q = row0 + (uint32_t)lane;
+        const uint32_t rel = R.rel[u], info = R.info[u];
+        const int co = (int)(16u * q - rel); // chunk start - packet start
+        const int re = (int)(info & 0xFFFFu);
+        const int rs = KIND == WC_KIND_PAYLOAD ? (int)((info >> 16) & 0xFFu) : 0;
+        const int lo = min(max(rs - co, 0), 16), hi = min(max(re - co, 0), 16);
+        const u32x4 keep = M.keep[lo * 17 + hi];
+        const u32x4 &d = R.d[u];
+        uint32_t E = 0, O = 0;
+        E = dot4(d.x, keep.x & 0x00FF00FFu, E);
+        O = dot4(d.x, keep.x & 0xFF00FF00u, O);
+        E = dot4(d.y, keep.y & 0x00FF00FFu, E);
+        O = dot4(d.y, keep.y & 0xFF00FF00u, O);
+        E = dot4(d.z, keep.z & 0x00FF00FFu, E);
+        O = dot4(d.z, keep.z & 0xFF00FF00u, O);
+        E = dot4(d.w, keep.w & 0x00FF00FFu, E);
+        O = dot4(d.w, keep.w & 0xFF00FF00u, O);
+        if constexpr (KIND == WC_KIND_PAYLOAD) {
+            if (co < 40) {
+                // Pseudo-header fields (in_cksum.c:149-151, 158-160), with
+                // the natural word weight of their byte position.
+                const bool v4 = (info >> 24) & 1u;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t h =
+                        v4 ? (dword_mask(9 - co, 10 - co, k) |
+                              dword_mask(12 - co, 20 - co, k))
+                           : (dword_mask(4 - co, 6 - co, k) |
+                              dword_mask(8 - co, 40 - co, k));
+                    E = dot4(pick_dword(d, k), kEvenW & h, E);
+                    O = dot4(pick_dword(d, k), kOddW & h, O);
+                }
+            }
+        }
+        uint32_t S = (rel & 1u) ? O + (E << 8) : E + (O << 8);
+        S = q < total ? S : 0u;
+        const uint32_t P = wave_incl_sum(S);
+        // Packet lane: Σ over its run [lo, hi) of this row.
+        const uint32_t rlo = max(cp, row0), rhi = min(ce, row0 + 64u);
+        const int last = (int)min(rhi - row0 - 1u, 63u);
+        const int before = (int)min(rlo - row0, 64u) - 1;
+        const uint32_t pe = __shfl(P, last, 64);
+        const uint32_t pb = __shfl(P, max(before, 0), 64);
+        if (rlo < rhi)
+            acc += pe - (before >= 0 ? pb : 0u);
+    }
+}
+
+template <int UN, int KIND, bool NT>
+__global__ void __launch_bounds__(256)
+k_cksum_flat(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
+             const uint16_t *__restrict__ lens, uint64_t n,
+             uint16_t *__restrict__ out, unsigned long long *__restrict__ bad)
+{
+    __shared__ FlatLds<UN> lds_all[kFlatWaves];
+    __shared__ FlatMaskLut lut;
+    build_mask_lut(lut);
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    FlatLds<UN> &L = lds_all[w];
+    const uint64_t ntiles = (n + 63) / 64;
+    const uint64_t nwaves = (uint64_t)gridDim.x * kFlatWaves;
+    uint64_t tile = (uint64_t)blockIdx.x * kFlatWaves + w;
+    uint32_t nbad = 0;
+
+    // Metadata of the first tile.
+    uint64_t p = tile * 64 + lane;
+    uint64_t off_n = p < n ? offs[p] : 0;
+    uint32_t len_n = p < n ? (uint32_t)lens[p] : 0u;
+
+    for (; tile < ntiles; tile += nwaves) {
+        p = tile * 64 + lane;
+        const bool valid = p < n;
+        const uint64_t off = off_n;
+        const uint32_t len = len_n;
+        {   // prefetch the next tile's metadata
+            const uint64_t pn = (tile + nwaves) * 64 + lane;
+            off_n = pn < n ? offs[pn] : 0;
+            len_n = pn < n ? (uint32_t)lens[pn] : 0u;
+        }
+        const uint64_t a = (uint64_t)base + off;
+        const uint32_t s = (uint32_t)(a & 15u);
+        const uint32_t span = KIND == WC_KIND_PAYLOAD ? max(len, 20u) : len;
+        const uint32_t nch = valid ? (s + span + 15u) >> 4 : 0u;
+
+        // payload_cksum: version / header length / special pseudo-header term
+        // of this lane's packet (in_cksum.c:142-160).
+        uint32_t hl = 0, v4 = 1, special = 0;
+        if constexpr (KIND == WC_KIND_PAYLOAD) {
+            if (valid) {
+                typedef const uint8_t __attribute__((address_space(1))) *gbyte;
+                gbyte h = (gbyte)(uintptr_t)a;
+                const uint32_t b0 = h[0], b2 = h[2], b3 = h[3], b6 = h[6];
+                v4 = (b0 >> 4) == 4u;
+                hl = v4 ? (b0 & 15u) * 4u : 40u;
+                if (v4) {
+                    const uint32_t x = (((b2 << 8) | b3) - hl) & 0xFFFFu;
+                    special = ((x & 0xFFu) << 8) | (x >> 8);
+                } else {
+                    special = b6 << 24;
+                }
+            }
+        }
+
+        // Chunk-slot range [cp, ce) of this lane's packet within the tile;
+        // rank among the tile's non-empty packets.
+        const uint32_t ce = wave_incl_sum(nch);
+        const uint32_t cp = ce - nch;
+        const uint32_t total = __shfl(ce, 63, 64);
+        const uint64_t nonempty = __ballot(nch != 0);
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
+            (uint32_t)(nonempty >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)nonempty, 0u));
+        const uint64_t vb = (a & ~15ull) - 16ull * cp;
+        if (nch != 0)
+            L.desc[rank] = FlatDesc{(uint32_t)vb, (uint32_t)(vb >> 32), s + 16u * cp,
+                                    len | (hl << 16) | (v4 << 24)};
+        // Row marks carry the row's number within the tile; reset them to a
+        // tag no row has so the previous tile's marks can't match.
+#pragma unroll
+        for (int r = 0; r < 2 * UN; ++r)
+            L.mark[r][lane] = 0xFFFFFFFFu;
+        wave_sync_lds();
+
+        uint32_t acc = special;
+        constexpr uint32_t kStep = 64u * UN;
+        if (total != 0) {
+            // Ping-pong row groups A / B (no register copies): group g+1's
+            // loads are in flight while group g is summed.
+            // No exit between the halves: a half past the tile's end sums
+            // zeros, and keeping each load's use in the next half stops
+            // hipcc from sinking the load next to its use.
+            FlatRows<UN> A, B;
+            flat_issue<UN, NT>(A, L, 0, lane, cp, ce, rank, total);
+            // sched_barrier keeps each issue phase ahead of the other
+            // group's accumulate (the scheduler would otherwise sink it).
+            for (uint32_t j = 0; j < total; j += 2 * kStep) {
+                flat_issue<UN, NT>(B, L, j + kStep, lane, cp, ce, rank, total);
+                __builtin_amdgcn_sched_barrier(0);
+                flat_accum<UN, KIND>(A, lut, j, lane, cp, ce, total, acc);
+                __builtin_amdgcn_sched_barrier(0);
+                flat_issue<UN, NT>(A, L, j + 2 * kStep, lane, cp, ce, rank, total);
+                __builtin_amdgcn_sched_barrier(0);
+                flat_accum<UN, KIND>(B, lut, j + kStep, lane, cp, ce, total, acc);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+
+        const uint16_t r = fold_not(acc);
+        if (valid && out)
+            out[p] = r;
+        nbad += valid && r != 0;
+        wave_sync_lds(); // the tables are rewritten by the next tile
+    }
+    if (bad) {
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1)
+            nbad += __shfl_xor(nbad, m, 64);
+        if (lane == 0 && nbad)
+            atomicAdd(bad, (unsigned long long)nbad);
+    }
+}
+
 // splitmix64 output k for state `seed` (must match oracle_synth_fill).
 __device__ __forceinline__ uint64_t splitmix64_at(uint64_t seed, uint64_t k)
 {
@@ -365,6 +672,49 @@ hipError_t launch_cksum(const LaunchArgs &a, const Shape &sh, int grid,
     WC_SHAPE_LIST
 #undef WC_SHAPE
     return hipErrorInvalidValue;
+}
+
+template <int UN>
+static hipError_t launch_flat_un(const LaunchArgs &a, hipStream_t st)
+{
+    const uint64_t tiles = (a.n + 63) / 64;
+    const uint64_t tpw = (uint64_t)(a.tiles_per_wave > 0 ? a.tiles_per_wave : 1);
+    const uint64_t waves = (tiles + tpw - 1) / tpw;
+    const int grid = (int)std::max<uint64_t>(1, (waves + kFlatWaves - 1) / kFlatWaves);
+    const uint8_t *b = (const uint8_t *)a.base;
+    unsigned long long *bad = (unsigned long long *)a.bad;
+#define WC_FLAT(K, N)                                                          \
+    hipLaunchKernelGGL((k_cksum_flat<UN, K, N>), dim3(grid), dim3(256), 0, st, \
+                       b, a.offs, a.lens, a.n, a.out, bad)
+    if (a.kind == WC_KIND_PAYLOAD) {
+        if (a.nontemporal)
+            WC_FLAT(WC_KIND_PAYLOAD, true);
+        else
+            WC_FLAT(WC_KIND_PAYLOAD, false);
+    } else {
+        if (a.nontemporal)
+            WC_FLAT(WC_KIND_IP, true);
+        else
+            WC_FLAT(WC_KIND_IP, false);
+    }
+#undef WC_FLAT
+    return hipGetLastError();
+}
+
+hipError_t launch_flat(const LaunchArgs &a, int unroll, hipStream_t st)
+{
+    switch (unroll) {
+    case 1:
+        return launch_flat_un<1>(a, st);
+    case 2:
+        return launch_flat_un<2>(a, st);
+    case 4:
+        return launch_flat_un<4>(a, st);
+    case 8:
+        return launch_flat_un<8>(a, st);
+    default:
+        return hipErrorInvalidValue;
+    }
 }
 
 hipError_t launch_synth(void *buf, uint64_t nbytes, uint64_t seed, int grid,
