@@ -63,6 +63,9 @@ def main():
     ap.add_argument("--variants", default="")
     ap.add_argument("--ceiling", action="store_true")
     ap.add_argument("--json", default="")
+    ap.add_argument("--kind", default="ip", choices=["ip", "payload"])
+    ap.add_argument("--offset", type=int, default=0, help="byte offset of packet 0 (c2/c3)")
+    ap.add_argument("--stride", type=int, default=0, help="packet stride (c2/c3; default len)")
     ap.add_argument("--ragged", action="store_true",
                     help="c2/c3 through the ragged entry point (offset/length arrays)")
     args = ap.parse_args()
@@ -79,19 +82,21 @@ def main():
         wc.synth_fill(buf, 1, nbytes=nbytes)
         d_off, d_len = torch.from_numpy(offs).to(dev), torch.from_numpy(lens).to(dev)
         out = torch.empty(n, dtype=torch.uint16, device=dev)
-        run = lambda: wc.cksum_ragged(buf, d_off, d_len, out=out)  # noqa: E731
+        run = lambda: wc.cksum_ragged(buf, d_off, d_len, out=out, kind=args.kind)  # noqa: E731
     else:
         L = 1472 if args.config == "c2" else args.len
         n = args.packets
+        stride = args.stride or L
         nbytes = n * L
-        buf = torch.empty(nbytes + 64, dtype=torch.uint8, device=dev)
-        wc.synth_fill(buf, 1, nbytes=nbytes)
+        buf = torch.empty(args.offset + n * stride + 64, dtype=torch.uint8, device=dev)
+        wc.synth_fill(buf, 1)
         out = torch.empty(n, dtype=torch.uint16, device=dev)
-        run = lambda: wc.cksum_strided(buf, L, L, n, out=out)  # noqa: E731
+        run = lambda: wc.cksum_strided(buf, stride, L, n, out=out, kind=args.kind,  # noqa: E731
+                                       byte_offset=args.offset)
         if args.ragged:
-            d_off = torch.arange(n, dtype=torch.int64, device=dev) * L
+            d_off = torch.arange(n, dtype=torch.int64, device=dev) * stride + args.offset
             d_len = torch.full((n,), L, dtype=torch.int16, device=dev)
-            run = lambda: wc.cksum_ragged(buf, d_off, d_len, out=out)  # noqa: E731
+            run = lambda: wc.cksum_ragged(buf, d_off, d_len, out=out, kind=args.kind)  # noqa: E731
 
     variants = [v.strip() for v in args.variants.split(";") if v.strip()] or [""]
     base_env = {k: os.environ.get(k) for k in ("WC_SHAPE", "WC_NT", "WC_BLOCKS_PER_CU", "WC_GRID",

@@ -222,9 +222,9 @@ Plan plan_ragged(const Device &D, uint64_t n)
 {
     Plan p;
     // Default: the chunk-balanced flat kernel (group = 0 marks it; unroll =
-    // 64-chunk rows in flight per lane).  WC_RAGGED=group selects the
+    // 64-chunk rows per ping-pong group).  WC_RAGGED=group selects the
     // group-per-packet kernel (shape from WC_SHAPE) for comparison.
-    p.shape = {0, 1, env_int("WC_FLAT_UN", 1)};
+    p.shape = {0, 1, env_int("WC_FLAT_UN", 2)};
     const char *mode = getenv("WC_RAGGED");
     if (mode && !strcmp(mode, "group")) {
         p.shape = {16, 2, 2};

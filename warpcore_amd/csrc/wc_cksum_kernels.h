@@ -67,9 +67,9 @@ struct Shape {
 
 hipError_t launch_cksum(const LaunchArgs &a, const Shape &sh, int grid,
                         hipStream_t st);
-// Chunk-balanced kernel for ragged batches (unroll = 64-chunk rows per lane
-// in flight: 1, 2, 4 or 8).
-hipError_t launch_flat(const LaunchArgs &a, int unroll, hipStream_t st);
+// Chunk-balanced kernel for ragged batches (rows = 64-chunk rows per
+// ping-pong group: 1, 2 or 4).
+hipError_t launch_flat(const LaunchArgs &a, int rows, hipStream_t st);
 hipError_t launch_synth(void *buf, uint64_t nbytes, uint64_t seed, int grid,
                         hipStream_t st);
 

@@ -344,16 +344,19 @@ struct FlatDesc {          // 16 bytes per non-empty packet of the tile, in LDS
     uint32_t info;         // len | hl << 16 | v4 << 24
 };
 
+// A row = 64 consecutive chunk slots, one per lane; a row group = UN rows
+// (slots row0 + 64u + lane), each load instruction fully coalesced.
 template <int UN>
 struct FlatRows {
     u32x4 d[UN];
-    uint32_t rel[UN], info[UN];
+    uint32_t own[UN];
 };
 
 template <int UN>
 struct FlatLds {
     FlatDesc desc[64];
-    uint32_t mark[2 * UN][64];
+    uint32_t mark[64];       // run-start tags of the row being issued
+    uint32_t pre[64 * UN];   // inclusive prefix sums of the group's chunk sums
 };
 
 // keep[lo * 17 + hi] = 0x01 in every byte b of a chunk with lo <= b < hi.
@@ -385,55 +388,61 @@ __device__ __forceinline__ void wave_sync_lds()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+__device__ __forceinline__ uint32_t mbcnt64(uint64_t m)
+{
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Owner lookup + loads for the UN rows of a group starting at slot g0.
 template <int UN, bool NT>
 __device__ __forceinline__ void flat_issue(FlatRows<UN> &R, FlatLds<UN> &L,
-                                           uint32_t j, int lane, uint32_t cp,
+                                           uint32_t g0, int lane, uint32_t cp,
                                            uint32_t ce, uint32_t rank,
-                                           uint32_t total)
+                                           uint32_t last_rank, uint32_t total)
 {
 #pragma unroll
     for (int u = 0; u < UN; ++u) {
-        const uint32_t row0 = j + 64u * u;
+        const uint32_t row0 = g0 + 64u * u;
         const uint32_t tag = row0 >> 6;
-        uint32_t *mark = L.mark[tag % (2 * UN)];
-        // Packet lane: its run inside this row is [lo, hi).
+        // Packet lane: its run inside this row is [lo, hi); a run that starts
+        // inside the row (not at its first slot) marks its first slot.
         const uint32_t lo = max(cp, row0), hi = min(ce, row0 + 64u);
         const bool part = lo < hi;
         if (part && lo > row0)
-            mark[lo - row0] = tag;
-        // Rank of the packet covering the row's first slot.
+            L.mark[lo - row0] = tag;
+        // Rank of the packet covering the row's first slot; a row past the
+        // tile's end has none and takes the last packet (its loads are
+        // clamped to the tile's last chunk, which that packet owns).
         const uint64_t firstm = __ballot(part && lo == row0);
-        const int fl = firstm ? (int)__builtin_ctzll(firstm) : 0;
-        const uint32_t first = __builtin_amdgcn_readlane(rank, fl);
+        const uint32_t first =
+            firstm ? __builtin_amdgcn_readlane(rank, (int)__builtin_ctzll(firstm))
+                   : last_rank;
         wave_sync_lds();
-        const bool start = mark[lane] == tag;
-        const uint64_t starts = __ballot(start);
-        const uint32_t below = __builtin_amdgcn_mbcnt_hi(
-            (uint32_t)(starts >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)starts, 0u));
-        const uint32_t owner = min(first + below + (start ? 1u : 0u), 63u);
-        const FlatDesc g = L.desc[owner];
-        R.rel[u] = g.rel;
-        R.info[u] = g.info;
+        const bool st = L.mark[lane] == tag;
+        const uint32_t own = min(first + mbcnt64(__ballot(st)) + (st ? 1u : 0u), last_rank);
+        R.own[u] = own;
+        const uint64_t vb = *reinterpret_cast<const uint64_t *>(&L.desc[own]);
         // Unconditional load (slots past the tile's end re-read its last
-        // chunk and are zeroed in flat_accum) keeps the issue stream
-        // straight-line, so hipcc can wait for exactly the older row group.
+        // chunk and are zeroed in flat_accum): a straight-line issue stream
+        // lets hipcc wait for exactly the older row group.
         const uint32_t q = min(row0 + (uint32_t)lane, total - 1u);
-        const uint64_t vb = ((uint64_t)g.vb_hi << 32) | g.vb_lo;
         R.d[u] = load_chunk<NT>(vb + 16ull * q);
     }
 }
 
 template <int UN, int KIND>
-__device__ __forceinline__ void flat_accum(const FlatRows<UN> &R,
-                                           const FlatMaskLut &M, uint32_t j,
+__device__ __forceinline__ void flat_accum(const FlatRows<UN> &R, FlatLds<UN> &L,
+                                           const FlatMaskLut &M, uint32_t g0,
                                            int lane, uint32_t cp, uint32_t ce,
                                            uint32_t total, uint32_t &acc)
 {
+    uint32_t carry = 0;
 #pragma unroll
     for (int u = 0; u < UN; ++u) {
-        const uint32_t row0 = j + 64u * u;
-        const uint32_t q = row0 + (uint32_t)lane;
-        const uint32_t rel = R.rel[u], info = R.info[u];
+        const uint32_t q = g0 + 64u * u + (uint32_t)lane;
+        const FlatDesc &g = L.desc[R.own[u]];
+        const uint32_t rel = g.rel, info = g.info;
         const int co = (int)(16u * q - rel); // chunk start - packet start
         const int re = (int)(info & 0xFFFFu);
         const int rs = KIND == WC_KIND_PAYLOAD ? (int)((info >> 16) & 0xFFu) : 0;
@@ -455,29 +464,36 @@ __device__ __forceinline__ void flat_accum(const FlatRows<UN> &R,
                 // the natural word weight of their byte position.
                 const bool v4 = (info >> 24) & 1u;
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
+                for (int j = 0; j < 4; ++j) {
                     const uint32_t h =
-                        v4 ? (dword_mask(9 - co, 10 - co, k) |
-                              dword_mask(12 - co, 20 - co, k))
-                           : (dword_mask(4 - co, 6 - co, k) |
-                              dword_mask(8 - co, 40 - co, k));
-                    E = dot4(pick_dword(d, k), kEvenW & h, E);
-                    O = dot4(pick_dword(d, k), kOddW & h, O);
+                        v4 ? (dword_mask(9 - co, 10 - co, j) |
+                              dword_mask(12 - co, 20 - co, j))
+                           : (dword_mask(4 - co, 6 - co, j) |
+                              dword_mask(8 - co, 40 - co, j));
+                    E = dot4(pick_dword(d, j), kEvenW & h, E);
+                    O = dot4(pick_dword(d, j), kOddW & h, O);
                 }
             }
         }
         uint32_t S = (rel & 1u) ? O + (E << 8) : E + (O << 8);
         S = q < total ? S : 0u;
-        const uint32_t P = wave_incl_sum(S);
-        // Packet lane: Σ over its run [lo, hi) of this row.
-        const uint32_t rlo = max(cp, row0), rhi = min(ce, row0 + 64u);
-        const int last = (int)min(rhi - row0 - 1u, 63u);
-        const int before = (int)min(rlo - row0, 64u) - 1;
-        const uint32_t pe = __shfl(P, last, 64);
-        const uint32_t pb = __shfl(P, max(before, 0), 64);
-        if (rlo < rhi)
-            acc += pe - (before >= 0 ? pb : 0u);
+        // Inclusive prefix over the group's slots, staged in LDS.
+        const uint32_t P = wave_incl_sum(S) + carry;
+        L.pre[64 * u + lane] = P;
+        if (u + 1 < UN)
+            carry = __builtin_amdgcn_readlane(P, 63);
     }
+    wave_sync_lds();
+    // Packet lane: Σ over its run [rlo, rhi) of the group.
+    constexpr uint32_t kGrp = 64u * UN;
+    const uint32_t rlo = max(cp, g0), rhi = min(ce, g0 + kGrp);
+    const uint32_t e_last = min(rhi - g0 - 1u, kGrp - 1u);
+    const uint32_t e_before = rlo > g0 ? min(rlo - g0 - 1u, kGrp - 1u) : 0u;
+    const uint32_t pe = L.pre[e_last];
+    const uint32_t pb = L.pre[e_before];
+    if (rlo < rhi)
+        acc += pe - (rlo > g0 ? pb : 0u);
+    wave_sync_lds(); // pre is rewritten by the next group
 }
 
 template <int UN, int KIND, bool NT>
@@ -544,39 +560,36 @@ k_cksum_flat(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
         const uint32_t cp = ce - nch;
         const uint32_t total = __shfl(ce, 63, 64);
         const uint64_t nonempty = __ballot(nch != 0);
-        const uint32_t rank = __builtin_amdgcn_mbcnt_hi(
-            (uint32_t)(nonempty >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)nonempty, 0u));
+        const uint32_t rank = mbcnt64(nonempty);
+        const uint32_t last_rank = nonempty ? (uint32_t)__builtin_popcountll(nonempty) - 1u : 0u;
         const uint64_t vb = (a & ~15ull) - 16ull * cp;
         if (nch != 0)
             L.desc[rank] = FlatDesc{(uint32_t)vb, (uint32_t)(vb >> 32), s + 16u * cp,
                                     len | (hl << 16) | (v4 << 24)};
         // Row marks carry the row's number within the tile; reset them to a
         // tag no row has so the previous tile's marks can't match.
-#pragma unroll
-        for (int r = 0; r < 2 * UN; ++r)
-            L.mark[r][lane] = 0xFFFFFFFFu;
+        L.mark[lane] = 0xFFFFFFFFu;
         wave_sync_lds();
 
         uint32_t acc = special;
-        constexpr uint32_t kStep = 64u * UN;
+        constexpr uint32_t kGrp = 64u * UN;
         if (total != 0) {
             // Ping-pong row groups A / B (no register copies): group g+1's
-            // loads are in flight while group g is summed.
-            // No exit between the halves: a half past the tile's end sums
-            // zeros, and keeping each load's use in the next half stops
-            // hipcc from sinking the load next to its use.
+            // loads are in flight while group g is summed.  No exit between
+            // the halves: a half past the tile's end sums zeros, and keeping
+            // each load's use in the next half stops hipcc sinking the load
+            // next to it; sched_barrier keeps each issue ahead of the other
+            // group's sum.
             FlatRows<UN> A, B;
-            flat_issue<UN, NT>(A, L, 0, lane, cp, ce, rank, total);
-            // sched_barrier keeps each issue phase ahead of the other
-            // group's accumulate (the scheduler would otherwise sink it).
-            for (uint32_t j = 0; j < total; j += 2 * kStep) {
-                flat_issue<UN, NT>(B, L, j + kStep, lane, cp, ce, rank, total);
+            flat_issue<UN, NT>(A, L, 0, lane, cp, ce, rank, last_rank, total);
+            for (uint32_t j = 0; j < total; j += 2 * kGrp) {
+                flat_issue<UN, NT>(B, L, j + kGrp, lane, cp, ce, rank, last_rank, total);
                 __builtin_amdgcn_sched_barrier(0);
-                flat_accum<UN, KIND>(A, lut, j, lane, cp, ce, total, acc);
+                flat_accum<UN, KIND>(A, L, lut, j, lane, cp, ce, total, acc);
                 __builtin_amdgcn_sched_barrier(0);
-                flat_issue<UN, NT>(A, L, j + 2 * kStep, lane, cp, ce, rank, total);
+                flat_issue<UN, NT>(A, L, j + 2 * kGrp, lane, cp, ce, rank, last_rank, total);
                 __builtin_amdgcn_sched_barrier(0);
-                flat_accum<UN, KIND>(B, lut, j + kStep, lane, cp, ce, total, acc);
+                flat_accum<UN, KIND>(B, L, lut, j + kGrp, lane, cp, ce, total, acc);
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
@@ -701,17 +714,15 @@ static hipError_t launch_flat_un(const LaunchArgs &a, hipStream_t st)
     return hipGetLastError();
 }
 
-hipError_t launch_flat(const LaunchArgs &a, int unroll, hipStream_t st)
+hipError_t launch_flat(const LaunchArgs &a, int rows, hipStream_t st)
 {
-    switch (unroll) {
+    switch (rows) {
     case 1:
         return launch_flat_un<1>(a, st);
     case 2:
         return launch_flat_un<2>(a, st);
     case 4:
         return launch_flat_un<4>(a, st);
-    case 8:
-        return launch_flat_un<8>(a, st);
     default:
         return hipErrorInvalidValue;
     }
