@@ -220,18 +220,14 @@ Plan plan_strided(const Device &D, uint64_t base, uint64_t stride, uint32_t len,
 
 Plan plan_ragged(const Device &D, uint64_t n)
 {
+    (void)D;
+    (void)n;
     Plan p;
-    // Default: the chunk-balanced flat kernel (group = 0 marks it; unroll =
-    // 64-chunk rows per ping-pong group).  WC_RAGGED=group selects the
-    // group-per-packet kernel (shape from WC_SHAPE) for comparison.
+    // The chunk-balanced flat kernel (group = 0 marks it; unroll = 64-chunk
+    // rows per ping-pong group, WC_FLAT_UN overrides).
     p.shape = {0, 1, env_int("WC_FLAT_UN", 2)};
-    const char *mode = getenv("WC_RAGGED");
-    if (mode && !strcmp(mode, "group")) {
-        p.shape = {16, 2, 2};
-        shape_override(&p.shape);
-    }
     p.full = false;
-    p.grid = p.shape.group ? grid_for(D, p.shape, n) : 0;
+    p.grid = 0;
     return p;
 }
 

@@ -9,35 +9,25 @@
 #define WC_KIND_PAYLOAD 1
 
 // Every (group width, chunk loads per lane, packets per group-iteration)
-// shape the planner may pick; each is instantiated for both kinds, strided /
-// ragged, masked / unmasked and temporal / nontemporal loads.
+// shape the strided planner may pick (wc_cksum_api.cpp: shape_for_chunks) or
+// WC_SHAPE may request; each is instantiated for ip_cksum (masked and
+// aligned-unmasked) and payload_cksum, with temporal and nontemporal loads.
 #define WC_SHAPE_LIST                                                          \
-    WC_SHAPE(4, 1, 4)                                                          \
     WC_SHAPE(4, 1, 8)                                                          \
     WC_SHAPE(4, 1, 16)                                                         \
     WC_SHAPE(8, 1, 4)                                                          \
     WC_SHAPE(8, 1, 8)                                                          \
-    WC_SHAPE(8, 2, 4)                                                          \
     WC_SHAPE(16, 1, 4)                                                         \
     WC_SHAPE(16, 1, 8)                                                         \
-    WC_SHAPE(16, 2, 2)                                                         \
     WC_SHAPE(16, 2, 4)                                                         \
-    WC_SHAPE(16, 3, 2)                                                         \
     WC_SHAPE(16, 3, 4)                                                         \
-    WC_SHAPE(16, 4, 2)                                                         \
-    WC_SHAPE(16, 6, 1)                                                         \
     WC_SHAPE(16, 6, 2)                                                         \
     WC_SHAPE(16, 6, 4)                                                         \
-    WC_SHAPE(32, 2, 1)                                                         \
-    WC_SHAPE(32, 3, 1)                                                         \
-    WC_SHAPE(32, 3, 2)                                                         \
     WC_SHAPE(32, 3, 4)                                                         \
     WC_SHAPE(32, 3, 8)                                                         \
     WC_SHAPE(32, 4, 1)                                                         \
     WC_SHAPE(32, 18, 1)                                                        \
-    WC_SHAPE(64, 2, 1)                                                         \
     WC_SHAPE(64, 4, 1)                                                         \
-    WC_SHAPE(64, 8, 1)                                                         \
     WC_SHAPE(64, 9, 1)                                                         \
     WC_SHAPE(64, 9, 2)
 
@@ -53,7 +43,7 @@ struct LaunchArgs {
     uint16_t *out;
     uint64_t *bad;
     int kind;
-    bool ragged;
+    bool ragged; // informational: ragged batches always use the flat kernel
     bool full;
     bool nontemporal;
     int tiles_per_wave; // flat kernel: 64-packet tiles each wave walks

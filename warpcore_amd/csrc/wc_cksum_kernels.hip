@@ -11,22 +11,22 @@
 //       pseudo-header, header layouts ip4.h:55-66 and ip6.h:45-57).
 //
 // Design:
-//   * A packet is owned by a GROUP of G lanes of one wave64 (G = 64 is "one
-//     packet per wavefront"; smaller packets pack 64/G packets per wave).
-//   * The group streams the packet's 16-byte-aligned chunks with one
-//     global_load_dwordx4 per lane per chunk (coalesced; an aligned 16-byte
-//     chunk that overlaps the packet never crosses a page, so covering
-//     [start & ~15, end) can't fault even at an allocation's edge).
+//   * Loads are always 16-byte-aligned chunks covering [start & ~15, end)
+//     (global_load_dwordx4 nt, coalesced).  An aligned chunk that overlaps the
+//     packet never crosses a page, so this can't fault at an allocation edge.
 //   * Each lane keeps two EXACT byte-lane sums with v_dot4_u32_u8: E = Σ bytes
-//     at even addresses, O = Σ bytes at odd addresses (masking and the IPv4 /
-//     IPv6 pseudo-header fields are folded into the dot4 byte weights).  The
-//     reference's uint32 accumulator is then exactly E + 256*O (packet starts
-//     at an even address) or O + 256*E (odd start), modulo 2^32 -- so results
-//     are bit-identical for every alignment, including the reference's uint32
-//     wrap-around on IPv6 next_hdr << 24 (in_cksum.c:157).
-//   * The group's partial sums are reduced with cross-lane adds, folded and
-//     complemented by the group leader, which stores the uint16.
-//   * No MFMA, no LDS tiles: this is a pure HBM-read stream (roofline: HBM).
+//     at even addresses, O = Σ bytes at odd addresses.  The reference's uint32
+//     accumulator is exactly E + 256*O (packet starts at an even address) or
+//     O + 256*E (odd start), modulo 2^32 -- bit-identical for every alignment,
+//     including the reference's uint32 wrap on IPv6 next_hdr << 24
+//     (in_cksum.c:157).  Head/tail masking and the pseudo-header fields
+//     payload_cksum adds with their natural word weight are dot4 byte weights,
+//     looked up in small LDS tables.
+//   * Strided batches: a GROUP of G lanes of one wave64 owns a packet (G = 64
+//     is "one packet per wavefront"), every lane issuing CPL x U loads before
+//     any arithmetic.  Ragged batches: the chunk-balanced flat kernel deals
+//     16-byte chunks, not packets, to lanes (section 4.3).
+//   * No MFMA: a pure HBM-read stream (roofline: HBM).
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -39,24 +39,16 @@ namespace wc {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-// dot4 byte weights: bytes 0 and 2 of a dword sit at even addresses (the
-// chunk base is 16-byte aligned), bytes 1 and 3 at odd addresses.
+// dot4 byte weights: bytes 0 and 2 of a dword sit at even addresses (chunks
+// are 16-byte aligned), bytes 1 and 3 at odd addresses.
 constexpr uint32_t kEvenW = 0x00010001u;
 constexpr uint32_t kOddW = 0x01000100u;
+constexpr uint32_t kEvenB = 0x00FF00FFu;
+constexpr uint32_t kOddB = 0xFF00FF00u;
 
 __device__ __forceinline__ uint32_t dot4(uint32_t x, uint32_t w, uint32_t acc)
 {
     return __builtin_amdgcn_udot4(x, w, acc, false);
-}
-
-// Byte mask (0xFF per selected byte) of the bytes of dword j (bytes 4j..4j+3
-// of a 16-byte chunk) that fall in [lo, hi), both relative to the chunk.
-__device__ __forceinline__ uint32_t dword_mask(int lo, int hi, int j)
-{
-    const int l = min(max(lo - 4 * j, 0), 4);
-    const int h = min(max(hi - 4 * j, 0), 4);
-    const uint64_t m = ((1ull << (8 * h)) - 1ull) & ~((1ull << (8 * l)) - 1ull);
-    return (uint32_t)m;
 }
 
 __device__ __forceinline__ uint32_t pick_dword(const u32x4 &d, int j)
@@ -72,6 +64,7 @@ __device__ __forceinline__ uint32_t pick_byte(const u32x4 &d, int pos)
 // Global (addrspace 1) pointer: lets hipcc emit global_load_dwordx4 rather
 // than flat loads for addresses computed as integers.
 typedef const u32x4 __attribute__((address_space(1))) *gchunk_ptr;
+typedef const uint8_t __attribute__((address_space(1))) *gbyte_ptr;
 
 template <bool NT>
 __device__ __forceinline__ u32x4 load_chunk(uint64_t addr)
@@ -91,6 +84,187 @@ __device__ __forceinline__ uint16_t fold_not(uint32_t s)
     return (uint16_t)~s;
 }
 
+// Exact reference accumulator of a lane's byte-lane sums (mod 2^32).
+__device__ __forceinline__ uint32_t combine(uint32_t E, uint32_t O, bool odd_start)
+{
+    return odd_start ? O + (E << 8) : E + (O << 8);
+}
+
+// payload_cksum's per-packet terms that are not byte-weighted sums
+// (in_cksum.c:142-160): version / header length from byte 0 (ip4.h:75-92),
+// IPv4 plen = bswap16(bswap16(ip->len) - hl) read as a native word
+// (152-153), IPv6 next_hdr << 24 (157).
+struct PseudoHdr {
+    uint32_t hl, v4, special;
+};
+
+__device__ __forceinline__ PseudoHdr pseudo_hdr(uint32_t b0, uint32_t b2,
+                                                uint32_t b3, uint32_t b6)
+{
+    PseudoHdr h;
+    h.v4 = (b0 >> 4) == 4u;
+    h.hl = h.v4 ? (b0 & 15u) * 4u : 40u;
+    if (h.v4) {
+        const uint32_t x = (((b2 << 8) | b3) - h.hl) & 0xFFFFu;
+        h.special = ((x & 0xFFu) << 8) | (x >> 8);
+    } else {
+        h.special = b6 << 24;
+    }
+    return h;
+}
+
+// ---------------------------------------------------------------------------
+// LDS weight tables.
+//
+// keep[lo * 17 + hi]    0x01 in byte b of a chunk iff lo <= b < hi
+// hdr[v4][co + 16]      0x01 in byte b iff packet offset co + b is one of the
+//                       pseudo-header fields payload_cksum adds with natural
+//                       word weight: IPv4 proto @9, src/dst @12..19
+//                       (in_cksum.c:149-151); IPv6 payload length @4..5,
+//                       src/dst @8..39 (158-160); co in [-16, 40), entry 56 = 0
+constexpr int kHdrSlots = 57;
+
+struct WeightLut {
+    u32x4 keep[17 * 17];
+    u32x4 hdr[2][kHdrSlots];
+};
+
+constexpr bool hdr_field(int v4, int o)
+{
+    return v4 ? (o == 9 || (o >= 12 && o < 20))
+              : (o == 4 || o == 5 || (o >= 8 && o < 40));
+}
+
+constexpr int kLutKeep = 17 * 17;
+constexpr int kLutAll = kLutKeep + 2 * kHdrSlots;
+
+struct WeightTable {
+    uint32_t w[kLutAll][4];
+};
+
+constexpr WeightTable make_weight_table()
+{
+    WeightTable t{};
+    for (int i = 0; i < kLutAll; ++i)
+        for (int j = 0; j < 4; ++j) {
+            uint32_t v = 0;
+            for (int b = 0; b < 4; ++b) {
+                const int pos = 4 * j + b;
+                bool on = false;
+                if (i < kLutKeep) {
+                    on = pos >= i / 17 && pos < i % 17;
+                } else {
+                    const int k = i - kLutKeep, v4 = k / kHdrSlots, slot = k % kHdrSlots;
+                    on = slot < kHdrSlots - 1 && hdr_field(v4, slot - 16 + pos);
+                }
+                v |= (on ? 1u : 0u) << (8 * b);
+            }
+            t.w[i][j] = v;
+        }
+    return t;
+}
+
+// Generated at compile time; each block copies it into LDS (6.4 KB).
+__device__ const WeightTable kWeightTable = make_weight_table();
+
+__device__ __forceinline__ void load_weight_lut(WeightLut &M)
+{
+    u32x4 *dst = reinterpret_cast<u32x4 *>(&M);
+    const u32x4 __attribute__((address_space(1))) *src =
+        (const u32x4 __attribute__((address_space(1))) *)&kWeightTable;
+    for (int i = threadIdx.x; i < kLutAll; i += blockDim.x)
+        dst[i] = src[i];
+}
+
+// Accumulate one 16-byte chunk whose start is `co` bytes after the packet
+// start: bytes at packet offsets [rs, re) get weight 1, and for
+// payload_cksum the pseudo-header field bytes get one more (so a malformed
+// IHL < 5 that makes the payload overlap src/dst double-counts them, as the
+// reference does).
+template <int KIND>
+__device__ __forceinline__ void accum_masked(const u32x4 &d, int co, int rs, int re,
+                                             uint32_t v4, const WeightLut &M,
+                                             uint32_t &E, uint32_t &O)
+{
+    const int lo = min(max(rs - co, 0), 16), hi = min(max(re - co, 0), 16);
+    u32x4 w = M.keep[lo * 17 + hi];
+    if constexpr (KIND == WC_KIND_PAYLOAD) {
+        const int slot = (co >= -16 && co < 40) ? co + 16 : kHdrSlots - 1;
+        w += M.hdr[v4][slot]; // byte weights <= 2: no carries between bytes
+    }
+    E = dot4(d.x, w.x & kEvenB, E);
+    O = dot4(d.x, w.x & kOddB, O);
+    E = dot4(d.y, w.y & kEvenB, E);
+    O = dot4(d.y, w.y & kOddB, O);
+    E = dot4(d.z, w.z & kEvenB, E);
+    O = dot4(d.z, w.z & kOddB, O);
+    E = dot4(d.w, w.w & kEvenB, E);
+    O = dot4(d.w, w.w & kOddB, O);
+}
+
+__device__ __forceinline__ void accum_full(const u32x4 &d, uint32_t &E, uint32_t &O)
+{
+    E = dot4(d.x, kEvenW, E);
+    O = dot4(d.x, kOddW, O);
+    E = dot4(d.y, kEvenW, E);
+    O = dot4(d.y, kOddW, O);
+    E = dot4(d.z, kEvenW, E);
+    O = dot4(d.z, kOddW, O);
+    E = dot4(d.w, kEvenW, E);
+    O = dot4(d.w, kOddW, O);
+}
+
+// Byte mask (0xFF per selected byte) of the bytes of dword j of a 16-byte
+// chunk that fall in [lo, hi), both relative to the chunk.
+__device__ __forceinline__ uint32_t dword_mask(int lo, int hi, int j)
+{
+    const int l = min(max(lo - 4 * j, 0), 4);
+    const int h = min(max(hi - 4 * j, 0), 4);
+    const uint64_t m = ((1ull << (8 * h)) - 1ull) & ~((1ull << (8 * l)) - 1ull);
+    return (uint32_t)m;
+}
+
+// accum_masked without tables (for the rare edge chunks of the strided
+// kernel): same weights, computed arithmetically.
+template <int KIND>
+__device__ __forceinline__ void accum_edge(const u32x4 &d, int co, int rs, int re,
+                                           uint32_t v4, uint32_t &E, uint32_t &O)
+{
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        uint32_t w = dword_mask(rs - co, re - co, j) & 0x01010101u;
+        if constexpr (KIND == WC_KIND_PAYLOAD) {
+            const uint32_t h = v4 ? (dword_mask(9 - co, 10 - co, j) |
+                                     dword_mask(12 - co, 20 - co, j))
+                                  : (dword_mask(4 - co, 6 - co, j) |
+                                     dword_mask(8 - co, 40 - co, j));
+            w += h & 0x01010101u;
+        }
+        const uint32_t x = pick_dword(d, j);
+        E = dot4(x, w & kEvenB, E);
+        O = dot4(x, w & kOddB, O);
+    }
+}
+
+// One chunk of the strided kernel: chunks strictly inside the summed range
+// (and past the header) take the full-weight path; the wave takes the edge
+// path only when one of its lanes holds a head / tail / header chunk.
+template <int KIND, bool FULL>
+__device__ __forceinline__ void accum_strided(const u32x4 &d, int co, int rs, int re,
+                                              uint32_t v4, uint32_t &E, uint32_t &O)
+{
+    if constexpr (FULL) {
+        accum_full(d, E, O);
+    } else {
+        const int head = KIND == WC_KIND_PAYLOAD ? max(rs, 40) : rs;
+        const bool edge = co < head || co + 16 > re;
+        if (__ballot(edge))
+            accum_edge<KIND>(d, co, rs, re, v4, E, O);
+        else
+            accum_full(d, E, O);
+    }
+}
+
 template <int G>
 __device__ __forceinline__ uint32_t group_sum(uint32_t v)
 {
@@ -100,72 +274,25 @@ __device__ __forceinline__ uint32_t group_sum(uint32_t v)
     return v;
 }
 
-// Accumulate one 16-byte chunk.  `co` = chunk start minus packet start (may be
-// negative for the first chunk of an unaligned packet); bytes whose packet
-// offset lies in [rs, re) get weight 1, and for payload_cksum the pseudo-header
-// fields that the reference adds with natural word weighting get one more.
-template <int KIND, bool FULL>
-__device__ __forceinline__ void accum_chunk(const u32x4 &d, int co, int rs,
-                                            int re, bool v4, uint32_t &E,
-                                            uint32_t &O)
-{
-    if constexpr (FULL) {
-        E = dot4(d.x, kEvenW, E);
-        O = dot4(d.x, kOddW, O);
-        E = dot4(d.y, kEvenW, E);
-        O = dot4(d.y, kOddW, O);
-        E = dot4(d.z, kEvenW, E);
-        O = dot4(d.z, kOddW, O);
-        E = dot4(d.w, kEvenW, E);
-        O = dot4(d.w, kOddW, O);
-    } else {
-        const int lo = rs - co, hi = re - co;
-        const bool hdr = KIND == WC_KIND_PAYLOAD && co < 40;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t m = dword_mask(lo, hi, j);
-            uint32_t we = kEvenW & m, wo = kOddW & m;
-            if (KIND == WC_KIND_PAYLOAD && hdr) {
-                // IPv4: proto @9 (reference adds p << 8, the natural weight of
-                // an odd byte), src/dst @12..19 (in_cksum.c:149-151).
-                // IPv6: payload length @4..5, src/dst @8..39
-                // (in_cksum.c:158-160).  Intervals within one version are
-                // disjoint, so OR-ing their masks is exact; adding to the
-                // range weight reproduces the reference's double count when a
-                // malformed IHL (< 5) makes the payload overlap src/dst.
-                const uint32_t h =
-                    v4 ? (dword_mask(9 - co, 10 - co, j) |
-                          dword_mask(12 - co, 20 - co, j))
-                       : (dword_mask(4 - co, 6 - co, j) |
-                          dword_mask(8 - co, 40 - co, j));
-                we += kEvenW & h;
-                wo += kOddW & h;
-            }
-            const uint32_t x = pick_dword(d, j);
-            E = dot4(x, we, E);
-            O = dot4(x, wo, O);
-        }
-    }
-}
-
-// Packet batch kernel.
+// ---------------------------------------------------------------------------
+// Strided batches: group-per-packet kernel.
 //   G     lanes per packet (power of two, 4..64)
 //   CPL   16-byte chunk loads per lane per pass (a pass covers G*CPL chunks)
 //   U     packets per group per iteration (more bytes in flight for small
 //         packets)
 //   KIND  WC_KIND_IP / WC_KIND_PAYLOAD
-//   RAGGED offsets/lengths from device arrays instead of i*stride / len
 //   FULL  every packet starts 16-byte aligned and len % 16 == 0 (IP only):
-//         no masks
+//         no masks, no tables
 //   NT    nontemporal loads
-template <int G, int CPL, int U, int KIND, bool RAGGED, bool FULL, bool NT>
+// Packet i is [base + i*stride, + len).  The grid is one-shot by default
+// (each wave does one iteration); a capped grid strides.
+template <int G, int CPL, int U, int KIND, bool FULL, bool NT>
 __global__ void __launch_bounds__(256)
-k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len_fixed,
-        const uint64_t *__restrict__ offs, const uint16_t *__restrict__ lens,
-        uint64_t n, uint16_t *__restrict__ out,
-        unsigned long long *__restrict__ bad)
+k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
+        uint64_t n, uint16_t *__restrict__ out, unsigned long long *__restrict__ bad)
 {
     static_assert(G >= 4 && G <= 64 && (G & (G - 1)) == 0, "group width");
+    static_assert(!(FULL && KIND == WC_KIND_PAYLOAD), "payload needs masks");
     constexpr int GPW = 64 / G;
     constexpr uint64_t PPW = (uint64_t)GPW * U;
     constexpr int PASS = G * CPL;
@@ -174,14 +301,16 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len_fixed,
     const int gl = lane & (G - 1);
     const int grp = lane / G;
     const int lead = lane & ~(G - 1);
-    const uint64_t wave =
-        (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    // payload_cksum reads the IPv4 header fields up to byte 19 even for a
+    // shorter len (in_cksum.c:149-151), so cover them too.
+    const uint32_t span = KIND == WC_KIND_PAYLOAD ? max(len, 20u) : len;
     uint32_t nbad = 0;
 
     for (uint64_t p0 = wave * PPW; p0 < n; p0 += nwaves * PPW) {
         uint64_t c0[U];
-        uint32_t nch[U], plen[U];
+        uint32_t nch[U];
         int s[U];
         bool valid[U];
         u32x4 d[U][CPL];
@@ -190,67 +319,43 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len_fixed,
         for (int u = 0; u < U; ++u) {
             const uint64_t i = p0 + (uint64_t)u * GPW + grp;
             valid[u] = i < n;
-            const uint64_t ii = valid[u] ? i : p0;
-            const uint64_t off = RAGGED ? offs[ii] : ii * stride;
-            const uint32_t l = RAGGED ? (uint32_t)lens[ii] : len_fixed;
-            const uint64_t a = (uint64_t)base + off;
-            // payload_cksum reads the IPv4 header fields up to byte 19 even
-            // for a shorter len (in_cksum.c:149-151), so cover them too.
-            const uint32_t span = KIND == WC_KIND_PAYLOAD ? max(l, 20u) : l;
-            plen[u] = l;
+            const uint64_t a = (uint64_t)base + (valid[u] ? i : p0) * stride;
             s[u] = (int)(a & 15u);
             c0[u] = a & ~15ull;
             nch[u] = valid[u] ? (uint32_t)((a + span + 15u - c0[u]) >> 4) : 0u;
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
+        for (int u = 0; u < U; ++u)
 #pragma unroll
             for (int c = 0; c < CPL; ++c) {
                 const uint32_t k = (uint32_t)(gl + c * G);
                 d[u][c] = k < nch[u] ? load_chunk<NT>(c0[u] + 16ull * k)
                                      : u32x4{0u, 0u, 0u, 0u};
             }
-        }
 
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            int rs = 0;
-            bool v4 = true;
-            uint32_t special = 0;
+            PseudoHdr ph{0u, 1u, 0u};
             if constexpr (KIND == WC_KIND_PAYLOAD) {
-                // Bytes 0, 2, 3, 6 of the header sit in the group's chunks 0/1,
-                // i.e. in d[u][0] of group lanes 0 and 1.
+                // Header bytes 0, 2, 3, 6 sit in the group's chunks 0/1, i.e.
+                // in d[u][0] of group lanes 0 and 1.
                 const int su = s[u];
-                const uint32_t b0 =
-                    __shfl(pick_byte(d[u][0], su & 15), lead + (su >> 4), 64);
+                const uint32_t b0 = __shfl(pick_byte(d[u][0], su), lead + (su >> 4), 64);
                 const uint32_t b2 = __shfl(pick_byte(d[u][0], (su + 2) & 15),
                                            lead + ((su + 2) >> 4), 64);
                 const uint32_t b3 = __shfl(pick_byte(d[u][0], (su + 3) & 15),
                                            lead + ((su + 3) >> 4), 64);
                 const uint32_t b6 = __shfl(pick_byte(d[u][0], (su + 6) & 15),
                                            lead + ((su + 6) >> 4), 64);
-                v4 = (b0 >> 4) == 4u;                        // ip4.h:75-79
-                const uint32_t hl = v4 ? (b0 & 15u) * 4u : 40u; // ip4.h:88-92
-                rs = (int)hl;
-                if (gl == 0) {
-                    if (v4) {
-                        // plen = bswap16(bswap16(ip->len) - hl) read as a
-                        // native word (in_cksum.c:152-153).
-                        const uint32_t x = (((b2 << 8) | b3) - hl) & 0xFFFFu;
-                        special = ((x & 0xFFu) << 8) | (x >> 8);
-                    } else {
-                        special = b6 << 24;                 // in_cksum.c:157
-                    }
-                }
+                ph = pseudo_hdr(b0, b2, b3, b6);
             }
-            const int re = (int)plen[u];
+            const int rs = (int)ph.hl, re = (int)len;
 
             uint32_t E = 0, O = 0;
 #pragma unroll
-            for (int c = 0; c < CPL; ++c) {
-                const int co = 16 * (gl + c * G) - s[u];
-                accum_chunk<KIND, FULL>(d[u][c], co, rs, re, v4, E, O);
-            }
+            for (int c = 0; c < CPL; ++c)
+                accum_strided<KIND, FULL>(d[u][c], 16 * (gl + c * G) - s[u], rs, re,
+                                          ph.v4, E, O);
             // Packets longer than one pass (e.g. 9000 B jumbo frames).
             for (uint32_t kb = PASS; kb < nch[u]; kb += PASS) {
                 u32x4 t[CPL];
@@ -261,21 +366,18 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len_fixed,
                                       : u32x4{0u, 0u, 0u, 0u};
                 }
 #pragma unroll
-                for (int c = 0; c < CPL; ++c) {
-                    const int co = 16 * (int)(kb + gl + c * G) - s[u];
-                    accum_chunk<KIND, FULL>(t[c], co, rs, re, v4, E, O);
-                }
+                for (int c = 0; c < CPL; ++c)
+                    accum_strided<KIND, FULL>(t[c], 16 * (int)(kb + gl + c * G) - s[u], rs,
+                                              re, ph.v4, E, O);
             }
 
-            // Exact reference accumulator, modulo 2^32 like its uint32.
-            uint32_t S = (s[u] & 1) ? O + (E << 8) : E + (O << 8);
-            S += special;
+            uint32_t S = combine(E, O, s[u] & 1);
+            S += gl == 0 ? ph.special : 0u;
             S = group_sum<G>(S);
             if (gl == 0 && valid[u]) {
                 const uint16_t r = fold_not(S);
-                const uint64_t i = p0 + (uint64_t)u * GPW + grp;
                 if (out)
-                    out[i] = r;
+                    out[p0 + (uint64_t)u * GPW + grp] = r;
                 nbad += r != 0;
             }
         }
@@ -304,14 +406,15 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len_fixed,
 //     clearing); a ballot of the marks gives the run starts, and
 //     rank(owner) = rank(first run) + mbcnt(starts at or below the lane);
 //   * the owner's descriptor (chunk base, start phase, length, header info)
-//     is one ds_read_b128 from the tile's LDS table, indexed by the rank of
-//     the packet among the tile's non-empty packets;
-//   * byte masks come from a 17 x 17 LDS table (bytes [lo, hi) of a chunk);
+//     comes from the tile's LDS table, indexed by the rank of the packet
+//     among the tile's non-empty packets;
+//   * byte weights come from the LDS tables above;
 //   * the lanes' exact partial sums go through a DPP inclusive prefix sum and
 //     each packet lane adds P[last slot] - P[first slot - 1] of its run to a
 //     register accumulator -- no atomics, no same-address LDS traffic.
-// Row groups of UN rows are double-buffered and the next tile's metadata is
-// prefetched while the current tile streams.
+// Row groups (UN interleaved rows, each load fully coalesced) are
+// ping-ponged, and the next tile's metadata (and, for payload_cksum, its
+// header bytes) is prefetched while the current tile streams.
 constexpr int kFlatWaves = 4; // 256-thread blocks
 
 // DPP controls (GFX9 family, gfx950 included).
@@ -338,47 +441,10 @@ __device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v)
     return v;
 }
 
-struct FlatDesc {          // 16 bytes per non-empty packet of the tile, in LDS
-    uint32_t vb_lo, vb_hi; // chunk q of the packet sits at vb + 16 q
-    uint32_t rel;          // packet start in the tile's slot-byte space
-    uint32_t info;         // len | hl << 16 | v4 << 24
-};
-
-// A row = 64 consecutive chunk slots, one per lane; a row group = UN rows
-// (slots row0 + 64u + lane), each load instruction fully coalesced.
-template <int UN>
-struct FlatRows {
-    u32x4 d[UN];
-    uint32_t own[UN];
-};
-
-template <int UN>
-struct FlatLds {
-    FlatDesc desc[64];
-    uint32_t mark[64];       // run-start tags of the row being issued
-    uint32_t pre[64 * UN];   // inclusive prefix sums of the group's chunk sums
-};
-
-// keep[lo * 17 + hi] = 0x01 in every byte b of a chunk with lo <= b < hi.
-struct FlatMaskLut {
-    u32x4 keep[17 * 17];
-};
-
-__device__ __forceinline__ void build_mask_lut(FlatMaskLut &M)
+__device__ __forceinline__ uint32_t mbcnt64(uint64_t m)
 {
-    for (int i = threadIdx.x; i < 17 * 17; i += blockDim.x) {
-        const int lo = i / 17, hi = i % 17;
-        uint32_t w[4];
-        for (int j = 0; j < 4; ++j) {
-            uint32_t v = 0;
-            for (int b = 0; b < 4; ++b) {
-                const int pos = 4 * j + b;
-                v |= (pos >= lo && pos < hi ? 1u : 0u) << (8 * b);
-            }
-            w[j] = v;
-        }
-        M.keep[i] = u32x4{w[0], w[1], w[2], w[3]};
-    }
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
 __device__ __forceinline__ void wave_sync_lds()
@@ -388,11 +454,24 @@ __device__ __forceinline__ void wave_sync_lds()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ uint32_t mbcnt64(uint64_t m)
-{
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                     __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
+struct FlatDesc {          // 16 bytes per non-empty packet of the tile, in LDS
+    uint32_t vb_lo, vb_hi; // chunk q of the packet sits at vb + 16 q
+    uint32_t rel;          // packet start in the tile's slot-byte space
+    uint32_t info;         // len | hl << 16 | v4 << 24
+};
+
+template <int UN>
+struct FlatRows {
+    u32x4 d[UN];
+    uint32_t own[UN];
+};
+
+template <int UN>
+struct FlatLds {
+    FlatDesc desc[64];
+    uint32_t mark[64];     // run-start tags of the row being issued
+    uint32_t pre[64 * UN]; // inclusive prefix sums of the group's chunk sums
+};
 
 // Owner lookup + loads for the UN rows of a group starting at slot g0.
 template <int UN, bool NT>
@@ -433,7 +512,7 @@ __device__ __forceinline__ void flat_issue(FlatRows<UN> &R, FlatLds<UN> &L,
 
 template <int UN, int KIND>
 __device__ __forceinline__ void flat_accum(const FlatRows<UN> &R, FlatLds<UN> &L,
-                                           const FlatMaskLut &M, uint32_t g0,
+                                           const WeightLut &M, uint32_t g0,
                                            int lane, uint32_t cp, uint32_t ce,
                                            uint32_t total, uint32_t &acc)
 {
@@ -443,40 +522,10 @@ __device__ __forceinline__ void flat_accum(const FlatRows<UN> &R, FlatLds<UN> &L
         const uint32_t q = g0 + 64u * u + (uint32_t)lane;
         const FlatDesc &g = L.desc[R.own[u]];
         const uint32_t rel = g.rel, info = g.info;
-        const int co = (int)(16u * q - rel); // chunk start - packet start
-        const int re = (int)(info & 0xFFFFu);
-        const int rs = KIND == WC_KIND_PAYLOAD ? (int)((info >> 16) & 0xFFu) : 0;
-        const int lo = min(max(rs - co, 0), 16), hi = min(max(re - co, 0), 16);
-        const u32x4 keep = M.keep[lo * 17 + hi];
-        const u32x4 &d = R.d[u];
         uint32_t E = 0, O = 0;
-        E = dot4(d.x, keep.x & 0x00FF00FFu, E);
-        O = dot4(d.x, keep.x & 0xFF00FF00u, O);
-        E = dot4(d.y, keep.y & 0x00FF00FFu, E);
-        O = dot4(d.y, keep.y & 0xFF00FF00u, O);
-        E = dot4(d.z, keep.z & 0x00FF00FFu, E);
-        O = dot4(d.z, keep.z & 0xFF00FF00u, O);
-        E = dot4(d.w, keep.w & 0x00FF00FFu, E);
-        O = dot4(d.w, keep.w & 0xFF00FF00u, O);
-        if constexpr (KIND == WC_KIND_PAYLOAD) {
-            if (co < 40) {
-                // Pseudo-header fields (in_cksum.c:149-151, 158-160), with
-                // the natural word weight of their byte position.
-                const bool v4 = (info >> 24) & 1u;
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const uint32_t h =
-                        v4 ? (dword_mask(9 - co, 10 - co, j) |
-                              dword_mask(12 - co, 20 - co, j))
-                           : (dword_mask(4 - co, 6 - co, j) |
-                              dword_mask(8 - co, 40 - co, j));
-                    E = dot4(pick_dword(d, j), kEvenW & h, E);
-                    O = dot4(pick_dword(d, j), kOddW & h, O);
-                }
-            }
-        }
-        uint32_t S = (rel & 1u) ? O + (E << 8) : E + (O << 8);
-        S = q < total ? S : 0u;
+        accum_masked<KIND>(R.d[u], (int)(16u * q - rel), (int)((info >> 16) & 0xFFu),
+                           (int)(info & 0xFFFFu), (info >> 24) & 1u, M, E, O);
+        const uint32_t S = q < total ? combine(E, O, rel & 1u) : 0u;
         // Inclusive prefix over the group's slots, staged in LDS.
         const uint32_t P = wave_incl_sum(S) + carry;
         L.pre[64 * u + lane] = P;
@@ -496,6 +545,15 @@ __device__ __forceinline__ void flat_accum(const FlatRows<UN> &R, FlatLds<UN> &L
     wave_sync_lds(); // pre is rewritten by the next group
 }
 
+// Header bytes 0, 2, 3, 6 of a packet (payload_cksum), packed b0 | b2 << 8 |
+// b3 << 16 | b6 << 24.
+__device__ __forceinline__ uint32_t load_hdr4(uint64_t a)
+{
+    gbyte_ptr h = (gbyte_ptr)(uintptr_t)a;
+    return (uint32_t)h[0] | ((uint32_t)h[2] << 8) | ((uint32_t)h[3] << 16) |
+           ((uint32_t)h[6] << 24);
+}
+
 template <int UN, int KIND, bool NT>
 __global__ void __launch_bounds__(256)
 k_cksum_flat(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
@@ -503,8 +561,8 @@ k_cksum_flat(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
              uint16_t *__restrict__ out, unsigned long long *__restrict__ bad)
 {
     __shared__ FlatLds<UN> lds_all[kFlatWaves];
-    __shared__ FlatMaskLut lut;
-    build_mask_lut(lut);
+    __shared__ WeightLut lut;
+    load_weight_lut(lut);
     __syncthreads();
 
     const int lane = threadIdx.x & 63;
@@ -515,44 +573,34 @@ k_cksum_flat(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
     uint64_t tile = (uint64_t)blockIdx.x * kFlatWaves + w;
     uint32_t nbad = 0;
 
-    // Metadata of the first tile.
+    // Metadata (and payload header bytes) of the first tile.
     uint64_t p = tile * 64 + lane;
     uint64_t off_n = p < n ? offs[p] : 0;
     uint32_t len_n = p < n ? (uint32_t)lens[p] : 0u;
+    uint32_t hdr_n = 0;
+    if constexpr (KIND == WC_KIND_PAYLOAD)
+        hdr_n = p < n ? load_hdr4((uint64_t)base + off_n) : 0u;
 
     for (; tile < ntiles; tile += nwaves) {
         p = tile * 64 + lane;
         const bool valid = p < n;
         const uint64_t off = off_n;
         const uint32_t len = len_n;
-        {   // prefetch the next tile's metadata
-            const uint64_t pn = (tile + nwaves) * 64 + lane;
-            off_n = pn < n ? offs[pn] : 0;
-            len_n = pn < n ? (uint32_t)lens[pn] : 0u;
-        }
+        const uint32_t hdr4 = hdr_n;
+        const uint64_t pn = (tile + nwaves) * 64 + lane;
+        const bool valid_n = pn < n;
+        off_n = valid_n ? offs[pn] : 0; // prefetch the next tile's metadata
+        len_n = valid_n ? (uint32_t)lens[pn] : 0u;
+
         const uint64_t a = (uint64_t)base + off;
         const uint32_t s = (uint32_t)(a & 15u);
         const uint32_t span = KIND == WC_KIND_PAYLOAD ? max(len, 20u) : len;
         const uint32_t nch = valid ? (s + span + 15u) >> 4 : 0u;
-
-        // payload_cksum: version / header length / special pseudo-header term
-        // of this lane's packet (in_cksum.c:142-160).
-        uint32_t hl = 0, v4 = 1, special = 0;
-        if constexpr (KIND == WC_KIND_PAYLOAD) {
-            if (valid) {
-                typedef const uint8_t __attribute__((address_space(1))) *gbyte;
-                gbyte h = (gbyte)(uintptr_t)a;
-                const uint32_t b0 = h[0], b2 = h[2], b3 = h[3], b6 = h[6];
-                v4 = (b0 >> 4) == 4u;
-                hl = v4 ? (b0 & 15u) * 4u : 40u;
-                if (v4) {
-                    const uint32_t x = (((b2 << 8) | b3) - hl) & 0xFFFFu;
-                    special = ((x & 0xFFu) << 8) | (x >> 8);
-                } else {
-                    special = b6 << 24;
-                }
-            }
-        }
+        PseudoHdr ph{0u, 1u, 0u};
+        if constexpr (KIND == WC_KIND_PAYLOAD)
+            if (valid)
+                ph = pseudo_hdr(hdr4 & 0xFFu, (hdr4 >> 8) & 0xFFu, (hdr4 >> 16) & 0xFFu,
+                                hdr4 >> 24);
 
         // Chunk-slot range [cp, ce) of this lane's packet within the tile;
         // rank among the tile's non-empty packets.
@@ -565,14 +613,21 @@ k_cksum_flat(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
         const uint64_t vb = (a & ~15ull) - 16ull * cp;
         if (nch != 0)
             L.desc[rank] = FlatDesc{(uint32_t)vb, (uint32_t)(vb >> 32), s + 16u * cp,
-                                    len | (hl << 16) | (v4 << 24)};
+                                    len | (ph.hl << 16) | (ph.v4 << 24)};
         // Row marks carry the row's number within the tile; reset them to a
         // tag no row has so the previous tile's marks can't match.
         L.mark[lane] = 0xFFFFFFFFu;
         wave_sync_lds();
 
-        uint32_t acc = special;
+        uint32_t acc = ph.special;
         constexpr uint32_t kGrp = 64u * UN;
+        FlatRows<UN> A, B;
+        if (total != 0)
+            flat_issue<UN, NT>(A, L, 0, lane, cp, ce, rank, last_rank, total);
+        // The next tile's header bytes: issued once its offsets are back,
+        // behind this tile's first loads.
+        if constexpr (KIND == WC_KIND_PAYLOAD)
+            hdr_n = valid_n ? load_hdr4((uint64_t)base + off_n) : 0u;
         if (total != 0) {
             // Ping-pong row groups A / B (no register copies): group g+1's
             // loads are in flight while group g is summed.  No exit between
@@ -580,8 +635,6 @@ k_cksum_flat(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
             // each load's use in the next half stops hipcc sinking the load
             // next to it; sched_barrier keeps each issue ahead of the other
             // group's sum.
-            FlatRows<UN> A, B;
-            flat_issue<UN, NT>(A, L, 0, lane, cp, ce, rank, last_rank, total);
             for (uint32_t j = 0; j < total; j += 2 * kGrp) {
                 flat_issue<UN, NT>(B, L, j + kGrp, lane, cp, ce, rank, last_rank, total);
                 __builtin_amdgcn_sched_barrier(0);
@@ -609,6 +662,9 @@ k_cksum_flat(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
     }
 }
 
+// ---------------------------------------------------------------------------
+// Synthetic bytes.
+
 // splitmix64 output k for state `seed` (must match oracle_synth_fill).
 __device__ __forceinline__ uint64_t splitmix64_at(uint64_t seed, uint64_t k)
 {
@@ -628,8 +684,7 @@ k_synth(uint8_t *__restrict__ buf, uint64_t nbytes, uint64_t seed)
     for (uint64_t w = 2 * tid; w < words; w += 2 * nth) {
         if (w + 1 < words) {
             uint64_t v[2] = {splitmix64_at(seed, w), splitmix64_at(seed, w + 1)};
-            *reinterpret_cast<u32x4 *>(buf + 8 * w) =
-                *reinterpret_cast<const u32x4 *>(v);
+            *reinterpret_cast<u32x4 *>(buf + 8 * w) = *reinterpret_cast<const u32x4 *>(v);
         } else {
             *reinterpret_cast<uint64_t *>(buf + 8 * w) = splitmix64_at(seed, w);
         }
@@ -644,12 +699,11 @@ k_synth(uint8_t *__restrict__ buf, uint64_t nbytes, uint64_t seed)
 // ---------------------------------------------------------------------------
 // Launch table.
 
-template <int G, int CPL, int U, int KIND, bool RAGGED, bool FULL, bool NT>
+template <int G, int CPL, int U, int KIND, bool FULL, bool NT>
 static hipError_t launch_one(const LaunchArgs &a, int grid, hipStream_t st)
 {
-    hipLaunchKernelGGL((k_cksum<G, CPL, U, KIND, RAGGED, FULL, NT>), dim3(grid),
-                       dim3(256), 0, st, (const uint8_t *)a.base, a.stride,
-                       a.len, a.offs, a.lens, a.n, a.out,
+    hipLaunchKernelGGL((k_cksum<G, CPL, U, KIND, FULL, NT>), dim3(grid), dim3(256), 0, st,
+                       (const uint8_t *)a.base, a.stride, a.len, a.n, a.out,
                        (unsigned long long *)a.bad);
     return hipGetLastError();
 }
@@ -658,26 +712,17 @@ template <int G, int CPL, int U>
 static hipError_t launch_shape(const LaunchArgs &a, int grid, hipStream_t st)
 {
     const bool nt = a.nontemporal;
-    if (a.kind == WC_KIND_PAYLOAD) {
-        if (a.ragged)
-            return nt ? launch_one<G, CPL, U, WC_KIND_PAYLOAD, true, false, true>(a, grid, st)
-                      : launch_one<G, CPL, U, WC_KIND_PAYLOAD, true, false, false>(a, grid, st);
-        return nt ? launch_one<G, CPL, U, WC_KIND_PAYLOAD, false, false, true>(a, grid, st)
-                  : launch_one<G, CPL, U, WC_KIND_PAYLOAD, false, false, false>(a, grid, st);
-    }
-    if (a.ragged)
-        return nt ? launch_one<G, CPL, U, WC_KIND_IP, true, false, true>(a, grid, st)
-                  : launch_one<G, CPL, U, WC_KIND_IP, true, false, false>(a, grid, st);
+    if (a.kind == WC_KIND_PAYLOAD)
+        return nt ? launch_one<G, CPL, U, WC_KIND_PAYLOAD, false, true>(a, grid, st)
+                  : launch_one<G, CPL, U, WC_KIND_PAYLOAD, false, false>(a, grid, st);
     if (a.full)
-        return nt ? launch_one<G, CPL, U, WC_KIND_IP, false, true, true>(a, grid, st)
-                  : launch_one<G, CPL, U, WC_KIND_IP, false, true, false>(a, grid, st);
-    return nt ? launch_one<G, CPL, U, WC_KIND_IP, false, false, true>(a, grid, st)
-              : launch_one<G, CPL, U, WC_KIND_IP, false, false, false>(a, grid, st);
+        return nt ? launch_one<G, CPL, U, WC_KIND_IP, true, true>(a, grid, st)
+                  : launch_one<G, CPL, U, WC_KIND_IP, true, false>(a, grid, st);
+    return nt ? launch_one<G, CPL, U, WC_KIND_IP, false, true>(a, grid, st)
+              : launch_one<G, CPL, U, WC_KIND_IP, false, false>(a, grid, st);
 }
 
-// The shapes the planner may choose (wc_cksum_plan.cpp keeps the same list).
-hipError_t launch_cksum(const LaunchArgs &a, const Shape &sh, int grid,
-                        hipStream_t st)
+hipError_t launch_cksum(const LaunchArgs &a, const Shape &sh, int grid, hipStream_t st)
 {
 #define WC_SHAPE(G_, C_, U_)                                                   \
     if (sh.group == G_ && sh.cpl == C_ && sh.unroll == U_)                     \
@@ -728,11 +773,9 @@ hipError_t launch_flat(const LaunchArgs &a, int rows, hipStream_t st)
     }
 }
 
-hipError_t launch_synth(void *buf, uint64_t nbytes, uint64_t seed, int grid,
-                        hipStream_t st)
+hipError_t launch_synth(void *buf, uint64_t nbytes, uint64_t seed, int grid, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_synth, dim3(grid), dim3(256), 0, st, (uint8_t *)buf,
-                       nbytes, seed);
+    hipLaunchKernelGGL(k_synth, dim3(grid), dim3(256), 0, st, (uint8_t *)buf, nbytes, seed);
     return hipGetLastError();
 }
 
