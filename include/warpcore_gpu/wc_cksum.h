@@ -77,6 +77,19 @@ int wc_verify_ragged(const void *d_base, const uint64_t *d_off,
                      const uint16_t *d_len, uint64_t n, uint16_t *d_out,
                      uint64_t *d_bad, int kind, void *stream);
 
+/* Fused IP + UDP pass over IP packets (each at its IP header, len = IP
+ * header + UDP length, as payload_cksum takes them): d_out_payload[i] =
+ * payload_cksum(pkt, len) and d_out_ip_hdr[i] = ip_cksum(pkt, ip4_hl(pkt[0]))
+ * -- the IPv4 header checksum mk_ip4_hdr / ip4_rx compute (ip4.c:184-186,
+ * 110-115) -- or 0 for an IPv6 packet, which has no header checksum
+ * (ip6.c:83-113).  One read of the packet bytes for both. */
+int wc_cksum_ip_udp_strided(const void *d_base, uint64_t stride, uint16_t len,
+                            uint64_t n, uint16_t *d_out_ip_hdr,
+                            uint16_t *d_out_payload, void *stream);
+int wc_cksum_ip_udp_ragged(const void *d_base, const uint64_t *d_off,
+                           const uint16_t *d_len, uint64_t n, uint16_t *d_out_ip_hdr,
+                           uint16_t *d_out_payload, void *stream);
+
 /* --- host-memory batch (end-to-end: pinned H2D, kernel, D2H) ------------- */
 
 /* Same as wc_cksum_ragged, but every buffer is host memory: the packet bytes

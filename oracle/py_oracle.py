@@ -54,3 +54,12 @@ def payload_sum(buf: bytes, length: int) -> int:
 def payload_cksum(buf: bytes, length: int | None = None) -> int:
     length = len(buf) if length is None else length
     return reduce16(payload_sum(buf, length))
+
+
+def ip_hdr_cksum(buf: bytes) -> int:
+    """What ip4_rx checks / mk_ip4_hdr stores: ip_cksum(ip, ip4_hl(vhl))
+    (ip4.c:110-115, 184-186) for IPv4; IPv6 has no header checksum -> 0."""
+    b = bytes(buf)
+    if b[0] >> 4 != 4:
+        return 0
+    return ip_cksum(b[: (b[0] & 0x0F) * 4])

@@ -5,13 +5,14 @@ Product: ``libwccksum.so`` (HIP kernels + C ABI, ``include/warpcore_gpu``).
 This package is the Python host mirror of that C ABI plus the synthetic
 packet generators and the multi-GPU shard driver used by bench.py.
 """
-from .cksum import (KIND_IP, KIND_PAYLOAD, WcError, cksum_host, cksum_ragged,
-                    cksum_strided, gpu_init, host_register, host_unregister,
+from .cksum import (KIND_IP, KIND_PAYLOAD, WcError, cksum_host, cksum_ip_udp_ragged,
+                    cksum_ip_udp_strided, cksum_ragged, cksum_strided, gpu_init, host_register, host_unregister,
                     ip_cksum, payload_cksum, plan_strided, synth_fill,
                     verify_ragged, verify_strided, version)
 
 __all__ = [
-    "KIND_IP", "KIND_PAYLOAD", "WcError", "cksum_host", "cksum_ragged",
+    "KIND_IP", "KIND_PAYLOAD", "WcError", "cksum_host", "cksum_ip_udp_ragged",
+    "cksum_ip_udp_strided", "cksum_ragged",
     "cksum_strided", "gpu_init", "host_register", "host_unregister", "ip_cksum",
     "payload_cksum", "plan_strided", "synth_fill", "verify_ragged",
     "verify_strided", "version",

@@ -30,6 +30,8 @@ SIGNATURES = {
     "wc_cksum_ragged": (_int, [_vp, _vp, _vp, _u64, _vp, _int, _vp]),
     "wc_verify_strided": (_int, [_vp, _u64, _u16, _u64, _vp, _vp, _int, _vp]),
     "wc_verify_ragged": (_int, [_vp, _vp, _vp, _u64, _vp, _vp, _int, _vp]),
+    "wc_cksum_ip_udp_strided": (_int, [_vp, _u64, _u16, _u64, _vp, _vp, _vp]),
+    "wc_cksum_ip_udp_ragged": (_int, [_vp, _vp, _vp, _u64, _vp, _vp, _vp]),
     "wc_cksum_host": (_int, [_vp, _u64, _vp, _vp, _u64, _vp, _int]),
     "wc_host_register": (_int, [_vp, _u64]),
     "wc_host_unregister": (_int, [_vp]),

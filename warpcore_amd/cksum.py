@@ -157,6 +157,30 @@ def verify_ragged(base, offsets, lengths, kind="payload", out=None,
     return out, bad
 
 
+def cksum_ip_udp_strided(base: torch.Tensor, stride: int, length: int, n: int,
+                        stream=None, byte_offset: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
+    """One pass over IP/UDP packets: (IPv4 header checksums, payload_cksum).
+    The header checksum is ip_cksum(ip, ip4_hl) (ip4.c:110-115, 184-186); 0
+    for IPv6 packets."""
+    hdr = _out_tensor(None, n, base.device)
+    pay = _out_tensor(None, n, base.device)
+    _check("wc_cksum_ip_udp_strided", _lib.load().wc_cksum_ip_udp_strided(
+        _dev_ptr(base) + byte_offset, stride, length, n, hdr.data_ptr(), pay.data_ptr(),
+        _stream_ptr(stream)))
+    return hdr, pay
+
+
+def cksum_ip_udp_ragged(base: torch.Tensor, offsets: torch.Tensor, lengths: torch.Tensor,
+                        stream=None) -> Tuple[torch.Tensor, torch.Tensor]:
+    n = offsets.numel()
+    hdr = _out_tensor(None, n, base.device)
+    pay = _out_tensor(None, n, base.device)
+    _check("wc_cksum_ip_udp_ragged", _lib.load().wc_cksum_ip_udp_ragged(
+        _dev_ptr(base), _dev_ptr(offsets), _dev_ptr(lengths), n, hdr.data_ptr(),
+        pay.data_ptr(), _stream_ptr(stream)))
+    return hdr, pay
+
+
 # --------------------------------------------------------------------------
 # Host-memory batches (end-to-end path).
 

@@ -243,7 +243,8 @@ int run(const Device &D, const wc::LaunchArgs &a, const Plan &p, hipStream_t st)
 }
 
 int batch_strided(const void *d_base, uint64_t stride, uint16_t len, uint64_t n,
-                  uint16_t *d_out, uint64_t *d_bad, int kind, void *stream)
+                  uint16_t *d_out, uint64_t *d_bad, int kind, void *stream,
+                  uint16_t *d_out_hdr = nullptr)
 {
     if (kind != WC_CKSUM_IP && kind != WC_CKSUM_PAYLOAD)
         return WC_EINVAL;
@@ -257,13 +258,14 @@ int batch_strided(const void *d_base, uint64_t stride, uint16_t len, uint64_t n,
         return rc;
     const Plan p = plan_strided(*D, (uint64_t)d_base, stride, len, n, kind);
     wc::LaunchArgs a{d_base, stride, len,  nullptr,  nullptr, n,
-                     d_out,  d_bad,  kind, false,    p.full,  nontemporal()};
+                     d_out,  d_bad,  kind, false,    p.full,  nontemporal(),
+                     0,      d_out_hdr};
     return run(*D, a, p, (hipStream_t)stream);
 }
 
 int batch_ragged(const void *d_base, const uint64_t *d_off, const uint16_t *d_len,
                  uint64_t n, uint16_t *d_out, uint64_t *d_bad, int kind,
-                 void *stream)
+                 void *stream, uint16_t *d_out_hdr = nullptr)
 {
     if (kind != WC_CKSUM_IP && kind != WC_CKSUM_PAYLOAD)
         return WC_EINVAL;
@@ -277,7 +279,8 @@ int batch_ragged(const void *d_base, const uint64_t *d_off, const uint16_t *d_le
         return rc;
     const Plan p = plan_ragged(*D, n);
     wc::LaunchArgs a{d_base, 0,     0,    d_off, d_len, n,
-                     d_out,  d_bad, kind, true,  false, nontemporal(), flat_tpw()};
+                     d_out,  d_bad, kind, true,  false, nontemporal(), flat_tpw(),
+                     d_out_hdr};
     return run(*D, a, p, (hipStream_t)stream);
 }
 
@@ -398,6 +401,26 @@ int wc_verify_ragged(const void *d_base, const uint64_t *d_off,
     if (!d_bad && n)
         return WC_EINVAL;
     return batch_ragged(d_base, d_off, d_len, n, d_out, d_bad, kind, stream);
+}
+
+int wc_cksum_ip_udp_strided(const void *d_base, uint64_t stride, uint16_t len,
+                            uint64_t n, uint16_t *d_out_ip_hdr,
+                            uint16_t *d_out_payload, void *stream)
+{
+    if (n && (!d_out_ip_hdr || !d_out_payload))
+        return WC_EINVAL;
+    return batch_strided(d_base, stride, len, n, d_out_payload, nullptr,
+                         WC_CKSUM_PAYLOAD, stream, d_out_ip_hdr);
+}
+
+int wc_cksum_ip_udp_ragged(const void *d_base, const uint64_t *d_off,
+                           const uint16_t *d_len, uint64_t n, uint16_t *d_out_ip_hdr,
+                           uint16_t *d_out_payload, void *stream)
+{
+    if (n && (!d_out_ip_hdr || !d_out_payload))
+        return WC_EINVAL;
+    return batch_ragged(d_base, d_off, d_len, n, d_out_payload, nullptr,
+                        WC_CKSUM_PAYLOAD, stream, d_out_ip_hdr);
 }
 
 int wc_host_register(void *h_ptr, uint64_t bytes)

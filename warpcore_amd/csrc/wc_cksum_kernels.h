@@ -47,6 +47,7 @@ struct LaunchArgs {
     bool full;
     bool nontemporal;
     int tiles_per_wave; // flat kernel: 64-packet tiles each wave walks
+    uint16_t *out_hdr;  // payload kind: also the IPv4 header checksums (or null)
 };
 
 struct Shape {

@@ -225,10 +225,13 @@ __device__ __forceinline__ uint32_t dword_mask(int lo, int hi, int j)
 }
 
 // accum_masked without tables (for the rare edge chunks of the strided
-// kernel): same weights, computed arithmetically.
-template <int KIND>
+// kernel): same weights, computed arithmetically.  With HDR, the bytes of the
+// IP header [0, hl) are also summed into (Eh, Oh) for the fused IPv4 header
+// checksum.
+template <int KIND, bool HDR>
 __device__ __forceinline__ void accum_edge(const u32x4 &d, int co, int rs, int re,
-                                           uint32_t v4, uint32_t &E, uint32_t &O)
+                                           uint32_t v4, uint32_t &E, uint32_t &O,
+                                           uint32_t &Eh, uint32_t &Oh)
 {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -243,15 +246,21 @@ __device__ __forceinline__ void accum_edge(const u32x4 &d, int co, int rs, int r
         const uint32_t x = pick_dword(d, j);
         E = dot4(x, w & kEvenB, E);
         O = dot4(x, w & kOddB, O);
+        if constexpr (HDR) {
+            const uint32_t m = dword_mask(-co, rs - co, j);
+            Eh = dot4(x, m & kEvenW, Eh);
+            Oh = dot4(x, m & kOddW, Oh);
+        }
     }
 }
 
 // One chunk of the strided kernel: chunks strictly inside the summed range
 // (and past the header) take the full-weight path; the wave takes the edge
 // path only when one of its lanes holds a head / tail / header chunk.
-template <int KIND, bool FULL>
+template <int KIND, bool FULL, bool HDR>
 __device__ __forceinline__ void accum_strided(const u32x4 &d, int co, int rs, int re,
-                                              uint32_t v4, uint32_t &E, uint32_t &O)
+                                              uint32_t v4, uint32_t &E, uint32_t &O,
+                                              uint32_t &Eh, uint32_t &Oh)
 {
     if constexpr (FULL) {
         accum_full(d, E, O);
@@ -259,7 +268,7 @@ __device__ __forceinline__ void accum_strided(const u32x4 &d, int co, int rs, in
         const int head = KIND == WC_KIND_PAYLOAD ? max(rs, 40) : rs;
         const bool edge = co < head || co + 16 > re;
         if (__ballot(edge))
-            accum_edge<KIND>(d, co, rs, re, v4, E, O);
+            accum_edge<KIND, HDR>(d, co, rs, re, v4, E, O, Eh, Oh);
         else
             accum_full(d, E, O);
     }
@@ -284,13 +293,17 @@ __device__ __forceinline__ uint32_t group_sum(uint32_t v)
 //   FULL  every packet starts 16-byte aligned and len % 16 == 0 (IP only):
 //         no masks, no tables
 //   NT    nontemporal loads
+//   HDR   (payload only) also store ip_cksum(ip, ip4_hl) of each IPv4 packet
+//         into out_hdr (0 for IPv6, which has no header checksum)
 // Packet i is [base + i*stride, + len).  The grid is one-shot by default
 // (each wave does one iteration); a capped grid strides.
-template <int G, int CPL, int U, int KIND, bool FULL, bool NT>
+template <int G, int CPL, int U, int KIND, bool FULL, bool NT, bool HDR>
 __global__ void __launch_bounds__(256)
 k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
-        uint64_t n, uint16_t *__restrict__ out, unsigned long long *__restrict__ bad)
+        uint64_t n, uint16_t *__restrict__ out, unsigned long long *__restrict__ bad,
+        uint16_t *__restrict__ out_hdr)
 {
+    static_assert(!HDR || KIND == WC_KIND_PAYLOAD, "header checksum rides on payload");
     static_assert(G >= 4 && G <= 64 && (G & (G - 1)) == 0, "group width");
     static_assert(!(FULL && KIND == WC_KIND_PAYLOAD), "payload needs masks");
     constexpr int GPW = 64 / G;
@@ -351,11 +364,11 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
             }
             const int rs = (int)ph.hl, re = (int)len;
 
-            uint32_t E = 0, O = 0;
+            uint32_t E = 0, O = 0, Eh = 0, Oh = 0;
 #pragma unroll
             for (int c = 0; c < CPL; ++c)
-                accum_strided<KIND, FULL>(d[u][c], 16 * (gl + c * G) - s[u], rs, re,
-                                          ph.v4, E, O);
+                accum_strided<KIND, FULL, HDR>(d[u][c], 16 * (gl + c * G) - s[u], rs, re,
+                                               ph.v4, E, O, Eh, Oh);
             // Packets longer than one pass (e.g. 9000 B jumbo frames).
             for (uint32_t kb = PASS; kb < nch[u]; kb += PASS) {
                 u32x4 t[CPL];
@@ -367,18 +380,24 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
                 }
 #pragma unroll
                 for (int c = 0; c < CPL; ++c)
-                    accum_strided<KIND, FULL>(t[c], 16 * (int)(kb + gl + c * G) - s[u], rs,
-                                              re, ph.v4, E, O);
+                    accum_strided<KIND, FULL, HDR>(t[c], 16 * (int)(kb + gl + c * G) - s[u],
+                                                   rs, re, ph.v4, E, O, Eh, Oh);
             }
 
             uint32_t S = combine(E, O, s[u] & 1);
             S += gl == 0 ? ph.special : 0u;
             S = group_sum<G>(S);
+            uint32_t Sh = 0;
+            if constexpr (HDR)
+                Sh = group_sum<G>(combine(Eh, Oh, s[u] & 1));
             if (gl == 0 && valid[u]) {
+                const uint64_t i = p0 + (uint64_t)u * GPW + grp;
                 const uint16_t r = fold_not(S);
                 if (out)
-                    out[p0 + (uint64_t)u * GPW + grp] = r;
+                    out[i] = r;
                 nbad += r != 0;
+                if constexpr (HDR)
+                    out_hdr[i] = ph.v4 ? fold_not(Sh) : 0; // ip4.c:110-115
             }
         }
     }
@@ -554,12 +573,32 @@ __device__ __forceinline__ uint32_t load_hdr4(uint64_t a)
            ((uint32_t)h[6] << 24);
 }
 
-template <int UN, int KIND, bool NT>
+// Fused IPv4 header checksum for the flat kernel: the packet's own lane sums
+// its header [0, hl) (at most 5 chunks) -- ip_cksum(ip, hl), ip4.c:110-115.
+template <bool NT>
+__device__ __forceinline__ uint16_t lane_hdr_cksum(uint64_t a, uint32_t hl,
+                                                   const WeightLut &M)
+{
+    const uint32_t s = (uint32_t)(a & 15u);
+    const uint64_t c0 = a & ~15ull;
+    const uint32_t nh = (s + hl + 15u) >> 4;
+    uint32_t E = 0, O = 0;
+    for (uint32_t k = 0; k < nh; ++k) {
+        const u32x4 d = load_chunk<false>(c0 + 16ull * k);
+        const int co = (int)(16u * k) - (int)s;
+        accum_masked<WC_KIND_IP>(d, co, 0, (int)hl, 0u, M, E, O);
+    }
+    return fold_not(combine(E, O, s & 1u));
+}
+
+template <int UN, int KIND, bool NT, bool HDR>
 __global__ void __launch_bounds__(256)
 k_cksum_flat(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
              const uint16_t *__restrict__ lens, uint64_t n,
-             uint16_t *__restrict__ out, unsigned long long *__restrict__ bad)
+             uint16_t *__restrict__ out, unsigned long long *__restrict__ bad,
+             uint16_t *__restrict__ out_hdr)
 {
+    static_assert(!HDR || KIND == WC_KIND_PAYLOAD, "header checksum rides on payload");
     __shared__ FlatLds<UN> lds_all[kFlatWaves];
     __shared__ WeightLut lut;
     load_weight_lut(lut);
@@ -651,6 +690,9 @@ k_cksum_flat(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
         if (valid && out)
             out[p] = r;
         nbad += valid && r != 0;
+        if constexpr (HDR)
+            if (valid)
+                out_hdr[p] = ph.v4 ? lane_hdr_cksum<NT>(a, ph.hl, lut) : 0;
         wave_sync_lds(); // the tables are rewritten by the next tile
     }
     if (bad) {
@@ -699,12 +741,12 @@ k_synth(uint8_t *__restrict__ buf, uint64_t nbytes, uint64_t seed)
 // ---------------------------------------------------------------------------
 // Launch table.
 
-template <int G, int CPL, int U, int KIND, bool FULL, bool NT>
+template <int G, int CPL, int U, int KIND, bool FULL, bool NT, bool HDR = false>
 static hipError_t launch_one(const LaunchArgs &a, int grid, hipStream_t st)
 {
-    hipLaunchKernelGGL((k_cksum<G, CPL, U, KIND, FULL, NT>), dim3(grid), dim3(256), 0, st,
-                       (const uint8_t *)a.base, a.stride, a.len, a.n, a.out,
-                       (unsigned long long *)a.bad);
+    hipLaunchKernelGGL((k_cksum<G, CPL, U, KIND, FULL, NT, HDR>), dim3(grid), dim3(256), 0,
+                       st, (const uint8_t *)a.base, a.stride, a.len, a.n, a.out,
+                       (unsigned long long *)a.bad, a.out_hdr);
     return hipGetLastError();
 }
 
@@ -712,6 +754,9 @@ template <int G, int CPL, int U>
 static hipError_t launch_shape(const LaunchArgs &a, int grid, hipStream_t st)
 {
     const bool nt = a.nontemporal;
+    if (a.kind == WC_KIND_PAYLOAD && a.out_hdr)
+        return nt ? launch_one<G, CPL, U, WC_KIND_PAYLOAD, false, true, true>(a, grid, st)
+                  : launch_one<G, CPL, U, WC_KIND_PAYLOAD, false, false, true>(a, grid, st);
     if (a.kind == WC_KIND_PAYLOAD)
         return nt ? launch_one<G, CPL, U, WC_KIND_PAYLOAD, false, true>(a, grid, st)
                   : launch_one<G, CPL, U, WC_KIND_PAYLOAD, false, false>(a, grid, st);
@@ -741,19 +786,24 @@ static hipError_t launch_flat_un(const LaunchArgs &a, hipStream_t st)
     const int grid = (int)std::max<uint64_t>(1, (waves + kFlatWaves - 1) / kFlatWaves);
     const uint8_t *b = (const uint8_t *)a.base;
     unsigned long long *bad = (unsigned long long *)a.bad;
-#define WC_FLAT(K, N)                                                          \
-    hipLaunchKernelGGL((k_cksum_flat<UN, K, N>), dim3(grid), dim3(256), 0, st, \
-                       b, a.offs, a.lens, a.n, a.out, bad)
-    if (a.kind == WC_KIND_PAYLOAD) {
+#define WC_FLAT(K, N, H)                                                       \
+    hipLaunchKernelGGL((k_cksum_flat<UN, K, N, H>), dim3(grid), dim3(256), 0,  \
+                       st, b, a.offs, a.lens, a.n, a.out, bad, a.out_hdr)
+    if (a.kind == WC_KIND_PAYLOAD && a.out_hdr) {
         if (a.nontemporal)
-            WC_FLAT(WC_KIND_PAYLOAD, true);
+            WC_FLAT(WC_KIND_PAYLOAD, true, true);
         else
-            WC_FLAT(WC_KIND_PAYLOAD, false);
+            WC_FLAT(WC_KIND_PAYLOAD, false, true);
+    } else if (a.kind == WC_KIND_PAYLOAD) {
+        if (a.nontemporal)
+            WC_FLAT(WC_KIND_PAYLOAD, true, false);
+        else
+            WC_FLAT(WC_KIND_PAYLOAD, false, false);
     } else {
         if (a.nontemporal)
-            WC_FLAT(WC_KIND_IP, true);
+            WC_FLAT(WC_KIND_IP, true, false);
         else
-            WC_FLAT(WC_KIND_IP, false);
+            WC_FLAT(WC_KIND_IP, false, false);
     }
 #undef WC_FLAT
     return hipGetLastError();
