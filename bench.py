@@ -11,8 +11,12 @@ path shards by packet with no data-path collective ("scaling": "weak"); ranks
 meet only at the barriers around the timed region and in the max-over-ranks
 time reduction.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4]
-                    [--len L] [--cpu-seconds S] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5]
+                    [--len L] [--kind ip|payload] [--cpu-seconds S] [--no-cpu-baseline]
+
+--config c5 is SURVEY C5 (strong scaling): 2^28 x 1472 B in total, split
+evenly over the ranks; a rank whose share exceeds its resident window (2^25
+packets = 49 GB) checksums it as several launches over that window.
 
 Rank 0 prints ONE JSON line (see DESIGN.md section 6 for every field).
 """
@@ -41,8 +45,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4"])
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"])
     ap.add_argument("--len", type=int, default=1472, help="packet bytes for c3")
+    ap.add_argument("--kind", default="ip", choices=["ip", "payload"],
+                    help="ip_cksum (default) or payload_cksum per packet")
+    ap.add_argument("--total-packets", type=int, default=1 << 28, help="c5 total")
+    ap.add_argument("--window-packets", type=int, default=1 << 25, help="c5 resident window")
     ap.add_argument("--packets", type=int, default=1 << 20)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -75,11 +83,35 @@ def dist_setup(args):
     return rank, dev_index, world, coll_dev
 
 
-def make_workload(args, dev, rank):
+def make_workload(args, dev, rank, world):
     import warpcore_amd as wc
+    from warpcore_amd import dist as wdist
     from warpcore_amd import synth
 
     seed = synth.SEED + rank
+    kind = args.kind
+    if args.config == "c5":
+        L = 1472
+        lo, hi = wdist.shard_range(args.total_packets, rank, world)
+        share = hi - lo
+        win = min(share, args.window_packets)
+        launches = (share + win - 1) // win
+        buf = torch.empty(win * L + 64, dtype=torch.uint8, device=dev)
+        wc.synth_fill(buf, seed, nbytes=win * L)
+        out = torch.empty(win, dtype=torch.uint16, device=dev)
+        counts = [min(win, share - k * win) for k in range(launches)]
+
+        def step():
+            for c in counts:
+                wc.cksum_strided(buf, L, L, c, out=out, kind=kind)
+
+        plan = wc.plan_strided(buf.data_ptr(), L, L, win, kind=kind)
+        desc = (f"C5: {args.total_packets} x {L} B in total, rank share {share} packets as "
+                f"{launches} launch(es) over a resident {win}-packet window")
+        meta = {"packets_total": args.total_packets, "packets_per_gpu": share,
+                "packet_bytes": L, "layout": "strided", "launches_per_step": launches,
+                "kind": kind}
+        return step, share, share * L, buf, out, plan, desc, meta, (L, L), "strong"
     if args.config in ("c2", "c3"):
         L = 1472 if args.config == "c2" else args.len
         n = args.packets
@@ -89,13 +121,13 @@ def make_workload(args, dev, rank):
         out = torch.empty(n, dtype=torch.uint16, device=dev)
 
         def step():
-            wc.cksum_strided(buf, L, L, n, out=out)
+            wc.cksum_strided(buf, L, L, n, out=out, kind=kind)
 
-        plan = wc.plan_strided(buf.data_ptr(), L, L, n)
+        plan = wc.plan_strided(buf.data_ptr(), L, L, n, kind=kind)
         desc = (f"C2: {n} x {L} B packets, stride {L}, device-resident"
                 if args.config == "c2" else f"C3: {n} x {L} B packets, stride {L}")
-        meta = {"packets_per_gpu": n, "packet_bytes": L, "layout": "strided"}
-        return step, n, nbytes, buf, out, plan, desc, meta, (L, L)
+        meta = {"packets_per_gpu": n, "packet_bytes": L, "layout": "strided", "kind": kind}
+        return step, n, nbytes, buf, out, plan, desc, meta, (L, L), "weak"
     # C4: Zipf(1) lengths 64..1472 B, packed with no padding (unaligned starts)
     n = 1 << 24 if args.packets == (1 << 20) else args.packets
     lens = synth.zipf_lengths(n, seed=synth.ZIPF_SEED + rank)
@@ -108,15 +140,15 @@ def make_workload(args, dev, rank):
     out = torch.empty(n, dtype=torch.uint16, device=dev)
 
     def step():
-        wc.cksum_ragged(buf, d_off, d_len, out=out)
+        wc.cksum_ragged(buf, d_off, d_len, out=out, kind=kind)
 
     desc = f"C4: {n} packets, Zipf(s=1) lengths 64-1472 B (mean {nbytes / n:.1f}), packed"
     meta = {"packets_per_gpu": n, "mean_packet_bytes": round(nbytes / n, 2),
-            "layout": "ragged"}
+            "layout": "ragged", "kind": kind}
     plan = {"kernel": "flat (chunk-balanced, 64-packet tiles)",
             "rows_in_flight": int(os.environ.get("WC_FLAT_UN", "1")),
             "grid": int((n + 255) // 256)}
-    return step, n, nbytes, buf, out, plan, desc, meta, (offs, lens)
+    return step, n, nbytes, buf, out, plan, desc, meta, (offs, lens), "weak"
 
 
 def cpu_baseline(args, buf, shape, nbytes_total):
@@ -124,13 +156,14 @@ def cpu_baseline(args, buf, shape, nbytes_total):
     from oracle import c_oracle  # checker / baseline only
 
     threads = c_oracle.default_threads()
-    if args.config in ("c2", "c3"):
+    k = 1 if args.kind == "payload" else 0
+    if args.config in ("c2", "c3", "c5"):
         L, stride = shape
         # The whole batch (DRAM-resident on the host, far beyond its L3),
         # repeated for >= --cpu-seconds.
         n_s = max(1, min(args.packets, (2 << 30) // L))
         sample = buf[: n_s * stride].cpu().numpy()
-        bps, passes = c_oracle.bench_strided(sample, stride, L, n_s, kind=0,
+        bps, passes = c_oracle.bench_strided(sample, stride, L, n_s, kind=k,
                                              threads=threads, min_seconds=args.cpu_seconds)
         desc = (f"{n_s} packets x {L} B ({n_s * L / 1e9:.2f} GB, the full batch), "
                 f"{passes} passes")
@@ -142,7 +175,7 @@ def cpu_baseline(args, buf, shape, nbytes_total):
         t0 = time.perf_counter()
         passes = 0
         while True:
-            c_oracle.cksum_ragged(sample, offs[:n_s], lens[:n_s], kind=0, threads=threads)
+            c_oracle.cksum_ragged(sample, offs[:n_s], lens[:n_s], kind=k, threads=threads)
             passes += 1
             if time.perf_counter() - t0 >= args.cpu_seconds:
                 break
@@ -158,18 +191,32 @@ def cpu_baseline(args, buf, shape, nbytes_total):
             f"one call per packet, {threads} pthreads on {model}"}
 
 
+def last_count(args):
+    from warpcore_amd import dist as wdist
+    rank, world = wdist.world()
+    lo, hi = wdist.shard_range(args.total_packets, rank, world)
+    share = hi - lo
+    win = min(share, args.window_packets)
+    return share - (share - 1) // win * win
+
+
 def parity_check(args, buf, out, shape, nbytes):
     """Bit-exact check of the last step's results over EVERY packet of the
     batch against the oracle (run outside the timed region)."""
     from oracle import c_oracle
+    k = 1 if args.kind == "payload" else 0
     got = out.cpu().numpy().view(np.uint16)
-    hb = buf[:nbytes].cpu().numpy()
-    if args.config in ("c2", "c3"):
+    hb = buf[: got.size * shape[1] if args.config != "c4" else nbytes].cpu().numpy()
+    if args.config in ("c2", "c3", "c5"):
+        # c5: the last launch of the step covered the window's first
+        # `counts[-1]` packets; check the whole window result of that launch
         L, stride = shape
-        want = c_oracle.cksum_strided(hb, stride, L, got.size, kind=0)
+        n_chk = got.size if args.config != "c5" else min(got.size, last_count(args))
+        want = c_oracle.cksum_strided(hb, stride, L, n_chk, kind=k)
+        got = got[:n_chk]
     else:
         offs, lens = shape
-        want = c_oracle.cksum_ragged(hb, offs, lens, kind=0)
+        want = c_oracle.cksum_ragged(hb, offs, lens, kind=k)
     return {"checked_packets": int(got.size), "mismatches": int((got != want).sum())}
 
 
@@ -181,7 +228,8 @@ def main():
     import warpcore_amd as wc
     wc.gpu_init(local)
 
-    step, n, nbytes, buf, out, plan, desc, meta, shape = make_workload(args, dev, rank)
+    step, n, nbytes, buf, out, plan, desc, meta, shape, scaling = make_workload(
+        args, dev, rank, world)
 
     for _ in range(args.warmup):
         step()
@@ -201,7 +249,7 @@ def main():
 
     elapsed = wdist.max_over_ranks(elapsed, coll_dev)
     kernel_ms_max = wdist.max_over_ranks(kernel_ms, coll_dev)
-    total_bytes = float(nbytes) * world * args.steps
+    total_bytes = float(wdist.sum_over_ranks(int(nbytes), coll_dev)) * args.steps
     value = total_bytes / elapsed / GIB
     achieved = nbytes / (kernel_ms * 1e-3) / 1e9  # GB/s of payload per launch (rank-local)
 
@@ -213,6 +261,8 @@ def main():
     try:
         tf = json.loads(Path(args.traffic_file).read_text())
         key = f"{args.config}:{meta.get('packet_bytes', 'zipf')}"
+        if args.kind != "ip":
+            key += f":{args.kind}"
         if key in tf:
             traffic = tf[key]["hbm_bytes_per_launch"]
     except (OSError, ValueError, KeyError):
@@ -232,7 +282,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic: splitmix64 payload bytes generated on device (wc_synth_fill)",

@@ -280,7 +280,7 @@ int batch_ragged(const void *d_base, const uint64_t *d_off, const uint16_t *d_le
     const Plan p = plan_ragged(*D, n);
     wc::LaunchArgs a{d_base, 0,     0,    d_off, d_len, n,
                      d_out,  d_bad, kind, true,  false, nontemporal(), flat_tpw(),
-                     d_out_hdr};
+                     d_out_hdr, env_int("WC_DIAG_NOLOAD", 0) != 0};
     return run(*D, a, p, (hipStream_t)stream);
 }
 

@@ -48,6 +48,7 @@ struct LaunchArgs {
     bool nontemporal;
     int tiles_per_wave; // flat kernel: 64-packet tiles each wave walks
     uint16_t *out_hdr;  // payload kind: also the IPv4 header checksums (or null)
+    bool diag_noload;   // WC_DIAG_NOLOAD=1: timing-only flat build (wrong results)
 };
 
 struct Shape {

@@ -493,7 +493,7 @@ struct FlatLds {
 };
 
 // Owner lookup + loads for the UN rows of a group starting at slot g0.
-template <int UN, bool NT>
+template <int UN, bool NT, bool NOLOAD = false>
 __device__ __forceinline__ void flat_issue(FlatRows<UN> &R, FlatLds<UN> &L,
                                            uint32_t g0, int lane, uint32_t cp,
                                            uint32_t ce, uint32_t rank,
@@ -525,7 +525,10 @@ __device__ __forceinline__ void flat_issue(FlatRows<UN> &R, FlatLds<UN> &L,
         // chunk and are zeroed in flat_accum): a straight-line issue stream
         // lets hipcc wait for exactly the older row group.
         const uint32_t q = min(row0 + (uint32_t)lane, total - 1u);
-        R.d[u] = load_chunk<NT>(vb + 16ull * q);
+        if constexpr (NOLOAD) // diagnostic build: same stream, no HBM traffic
+            R.d[u] = u32x4{(uint32_t)vb, q, (uint32_t)(vb >> 32), q ^ 0x5a5a5a5au};
+        else
+            R.d[u] = load_chunk<NT>(vb + 16ull * q);
     }
 }
 
@@ -591,7 +594,7 @@ __device__ __forceinline__ uint16_t lane_hdr_cksum(uint64_t a, uint32_t hl,
     return fold_not(combine(E, O, s & 1u));
 }
 
-template <int UN, int KIND, bool NT, bool HDR>
+template <int UN, int KIND, bool NT, bool HDR, bool NOLOAD = false>
 __global__ void __launch_bounds__(256)
 k_cksum_flat(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
              const uint16_t *__restrict__ lens, uint64_t n,
@@ -662,7 +665,7 @@ k_cksum_flat(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
         constexpr uint32_t kGrp = 64u * UN;
         FlatRows<UN> A, B;
         if (total != 0)
-            flat_issue<UN, NT>(A, L, 0, lane, cp, ce, rank, last_rank, total);
+            flat_issue<UN, NT, NOLOAD>(A, L, 0, lane, cp, ce, rank, last_rank, total);
         // The next tile's header bytes: issued once its offsets are back,
         // behind this tile's first loads.
         if constexpr (KIND == WC_KIND_PAYLOAD)
@@ -675,11 +678,11 @@ k_cksum_flat(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
             // next to it; sched_barrier keeps each issue ahead of the other
             // group's sum.
             for (uint32_t j = 0; j < total; j += 2 * kGrp) {
-                flat_issue<UN, NT>(B, L, j + kGrp, lane, cp, ce, rank, last_rank, total);
+                flat_issue<UN, NT, NOLOAD>(B, L, j + kGrp, lane, cp, ce, rank, last_rank, total);
                 __builtin_amdgcn_sched_barrier(0);
                 flat_accum<UN, KIND>(A, L, lut, j, lane, cp, ce, total, acc);
                 __builtin_amdgcn_sched_barrier(0);
-                flat_issue<UN, NT>(A, L, j + 2 * kGrp, lane, cp, ce, rank, last_rank, total);
+                flat_issue<UN, NT, NOLOAD>(A, L, j + 2 * kGrp, lane, cp, ce, rank, last_rank, total);
                 __builtin_amdgcn_sched_barrier(0);
                 flat_accum<UN, KIND>(B, L, lut, j + kGrp, lane, cp, ce, total, acc);
                 __builtin_amdgcn_sched_barrier(0);
@@ -789,6 +792,11 @@ static hipError_t launch_flat_un(const LaunchArgs &a, hipStream_t st)
 #define WC_FLAT(K, N, H)                                                       \
     hipLaunchKernelGGL((k_cksum_flat<UN, K, N, H>), dim3(grid), dim3(256), 0,  \
                        st, b, a.offs, a.lens, a.n, a.out, bad, a.out_hdr)
+    if (a.diag_noload && a.kind == WC_KIND_IP) {
+        hipLaunchKernelGGL((k_cksum_flat<UN, WC_KIND_IP, true, false, true>), dim3(grid),
+                           dim3(256), 0, st, b, a.offs, a.lens, a.n, a.out, bad, a.out_hdr);
+        return hipGetLastError();
+    }
     if (a.kind == WC_KIND_PAYLOAD && a.out_hdr) {
         if (a.nontemporal)
             WC_FLAT(WC_KIND_PAYLOAD, true, true);
