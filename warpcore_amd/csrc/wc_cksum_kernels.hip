@@ -116,7 +116,7 @@ __device__ __forceinline__ PseudoHdr pseudo_hdr(uint32_t b0, uint32_t b2,
 // ---------------------------------------------------------------------------
 // LDS weight tables.
 //
-// keep[lo * 17 + hi]    0x01 in byte b of a chunk iff lo <= b < hi
+// keep[lo * 17 + hi]    0xFF in byte b of a chunk iff lo <= b < hi
 // hdr[v4][co + 16]      0x01 in byte b iff packet offset co + b is one of the
 //                       pseudo-header fields payload_cksum adds with natural
 //                       word weight: IPv4 proto @9, src/dst @12..19
@@ -157,7 +157,7 @@ constexpr WeightTable make_weight_table()
                     const int k = i - kLutKeep, v4 = k / kHdrSlots, slot = k % kHdrSlots;
                     on = slot < kHdrSlots - 1 && hdr_field(v4, slot - 16 + pos);
                 }
-                v |= (on ? 1u : 0u) << (8 * b);
+                v |= (on ? (i < kLutKeep ? 0xFFu : 1u) : 0u) << (8 * b);
             }
             t.w[i][j] = v;
         }
@@ -187,19 +187,30 @@ __device__ __forceinline__ void accum_masked(const u32x4 &d, int co, int rs, int
                                              uint32_t &E, uint32_t &O)
 {
     const int lo = min(max(rs - co, 0), 16), hi = min(max(re - co, 0), 16);
-    u32x4 w = M.keep[lo * 17 + hi];
+    const u32x4 keep = M.keep[lo * 17 + hi];
     if constexpr (KIND == WC_KIND_PAYLOAD) {
         const int slot = (co >= -16 && co < 40) ? co + 16 : kHdrSlots - 1;
-        w += M.hdr[v4][slot]; // byte weights <= 2: no carries between bytes
+        // byte weights <= 2: no carries between bytes
+        const u32x4 w = (keep & 0x01010101u) + M.hdr[v4][slot];
+        E = dot4(d.x, w.x & kEvenB, E);
+        O = dot4(d.x, w.x & kOddB, O);
+        E = dot4(d.y, w.y & kEvenB, E);
+        O = dot4(d.y, w.y & kOddB, O);
+        E = dot4(d.z, w.z & kEvenB, E);
+        O = dot4(d.z, w.z & kOddB, O);
+        E = dot4(d.w, w.w & kEvenB, E);
+        O = dot4(d.w, w.w & kOddB, O);
+    } else {
+        const u32x4 m = d & keep; // masked bytes, then the fixed byte-lane weights
+        E = dot4(m.x, kEvenW, E);
+        O = dot4(m.x, kOddW, O);
+        E = dot4(m.y, kEvenW, E);
+        O = dot4(m.y, kOddW, O);
+        E = dot4(m.z, kEvenW, E);
+        O = dot4(m.z, kOddW, O);
+        E = dot4(m.w, kEvenW, E);
+        O = dot4(m.w, kOddW, O);
     }
-    E = dot4(d.x, w.x & kEvenB, E);
-    O = dot4(d.x, w.x & kOddB, O);
-    E = dot4(d.y, w.y & kEvenB, E);
-    O = dot4(d.y, w.y & kOddB, O);
-    E = dot4(d.z, w.z & kEvenB, E);
-    O = dot4(d.z, w.z & kOddB, O);
-    E = dot4(d.w, w.w & kEvenB, E);
-    O = dot4(d.w, w.w & kOddB, O);
 }
 
 __device__ __forceinline__ void accum_full(const u32x4 &d, uint32_t &E, uint32_t &O)
@@ -466,13 +477,6 @@ __device__ __forceinline__ uint32_t mbcnt64(uint64_t m)
                                      __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-__device__ __forceinline__ void wave_sync_lds()
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 struct FlatDesc {          // 16 bytes per non-empty packet of the tile, in LDS
     uint32_t vb_lo, vb_hi; // chunk q of the packet sits at vb + 16 q
     uint32_t rel;          // packet start in the tile's slot-byte space
@@ -488,9 +492,16 @@ struct FlatRows {
 template <int UN>
 struct FlatLds {
     FlatDesc desc[64];
-    uint32_t mark[64];     // run-start tags of the row being issued
+    uint32_t mark[UN][64]; // run-start tags, one array per row of a group
     uint32_t pre[64 * UN]; // inclusive prefix sums of the group's chunk sums
 };
+
+// Intra-wave LDS hand-offs need no fence: one wave's LDS instructions execute
+// in issue order.  wave_barrier only stops hipcc moving LDS accesses across.
+__device__ __forceinline__ void wave_order()
+{
+    __builtin_amdgcn_wave_barrier();
+}
 
 // Owner lookup + loads for the UN rows of a group starting at slot g0.
 template <int UN, bool NT, bool NOLOAD = false>
@@ -499,26 +510,30 @@ __device__ __forceinline__ void flat_issue(FlatRows<UN> &R, FlatLds<UN> &L,
                                            uint32_t ce, uint32_t rank,
                                            uint32_t last_rank, uint32_t total)
 {
+    uint32_t first[UN];
 #pragma unroll
     for (int u = 0; u < UN; ++u) {
         const uint32_t row0 = g0 + 64u * u;
-        const uint32_t tag = row0 >> 6;
         // Packet lane: its run inside this row is [lo, hi); a run that starts
-        // inside the row (not at its first slot) marks its first slot.
+        // inside the row (not at its first slot) marks its first slot with
+        // the row's tag.
         const uint32_t lo = max(cp, row0), hi = min(ce, row0 + 64u);
         const bool part = lo < hi;
         if (part && lo > row0)
-            L.mark[lo - row0] = tag;
+            L.mark[u][lo - row0] = row0 >> 6;
         // Rank of the packet covering the row's first slot; a row past the
         // tile's end has none and takes the last packet (its loads are
         // clamped to the tile's last chunk, which that packet owns).
         const uint64_t firstm = __ballot(part && lo == row0);
-        const uint32_t first =
-            firstm ? __builtin_amdgcn_readlane(rank, (int)__builtin_ctzll(firstm))
-                   : last_rank;
-        wave_sync_lds();
-        const bool st = L.mark[lane] == tag;
-        const uint32_t own = min(first + mbcnt64(__ballot(st)) + (st ? 1u : 0u), last_rank);
+        first[u] = firstm ? __builtin_amdgcn_readlane(rank, (int)__builtin_ctzll(firstm))
+                          : last_rank;
+    }
+    wave_order();
+#pragma unroll
+    for (int u = 0; u < UN; ++u) {
+        const uint32_t row0 = g0 + 64u * u;
+        const bool st = L.mark[u][lane] == (row0 >> 6);
+        const uint32_t own = min(first[u] + mbcnt64(__ballot(st)) + (st ? 1u : 0u), last_rank);
         R.own[u] = own;
         const uint64_t vb = *reinterpret_cast<const uint64_t *>(&L.desc[own]);
         // Unconditional load (slots past the tile's end re-read its last
@@ -538,7 +553,7 @@ __device__ __forceinline__ void flat_accum(const FlatRows<UN> &R, FlatLds<UN> &L
                                            int lane, uint32_t cp, uint32_t ce,
                                            uint32_t total, uint32_t &acc)
 {
-    uint32_t carry = 0;
+    uint32_t P[UN];
 #pragma unroll
     for (int u = 0; u < UN; ++u) {
         const uint32_t q = g0 + 64u * u + (uint32_t)lane;
@@ -547,14 +562,27 @@ __device__ __forceinline__ void flat_accum(const FlatRows<UN> &R, FlatLds<UN> &L
         uint32_t E = 0, O = 0;
         accum_masked<KIND>(R.d[u], (int)(16u * q - rel), (int)((info >> 16) & 0xFFu),
                            (int)(info & 0xFFFFu), (info >> 24) & 1u, M, E, O);
-        const uint32_t S = q < total ? combine(E, O, rel & 1u) : 0u;
-        // Inclusive prefix over the group's slots, staged in LDS.
-        const uint32_t P = wave_incl_sum(S) + carry;
-        L.pre[64 * u + lane] = P;
-        if (u + 1 < UN)
-            carry = __builtin_amdgcn_readlane(P, 63);
+        P[u] = q < total ? combine(E, O, rel & 1u) : 0u;
     }
-    wave_sync_lds();
+    // Inclusive prefix sums of the UN rows, step-interleaved so each row's DPP
+    // step fills the others' hazard slots; then the rows are chained.
+#define WC_SCAN_STEP(CTRL, ROWS)                                               \
+    _Pragma("unroll") for (int u = 0; u < UN; ++u) P[u] += dpp0<CTRL, ROWS>(P[u]);
+    WC_SCAN_STEP(kDppRowShr + 1, 0xF)
+    WC_SCAN_STEP(kDppRowShr + 2, 0xF)
+    WC_SCAN_STEP(kDppRowShr + 4, 0xF)
+    WC_SCAN_STEP(kDppRowShr + 8, 0xF)
+    WC_SCAN_STEP(kDppRowBcast15, 0xA)
+    WC_SCAN_STEP(kDppRowBcast31, 0xC)
+#undef WC_SCAN_STEP
+    uint32_t carry = 0;
+#pragma unroll
+    for (int u = 0; u < UN; ++u) {
+        const uint32_t tot = __builtin_amdgcn_readlane(P[u], 63);
+        L.pre[64 * u + lane] = P[u] + carry;
+        carry += tot;
+    }
+    wave_order();
     // Packet lane: Σ over its run [rlo, rhi) of the group.
     constexpr uint32_t kGrp = 64u * UN;
     const uint32_t rlo = max(cp, g0), rhi = min(ce, g0 + kGrp);
@@ -564,7 +592,7 @@ __device__ __forceinline__ void flat_accum(const FlatRows<UN> &R, FlatLds<UN> &L
     const uint32_t pb = L.pre[e_before];
     if (rlo < rhi)
         acc += pe - (rlo > g0 ? pb : 0u);
-    wave_sync_lds(); // pre is rewritten by the next group
+    wave_order(); // pre is rewritten by the next group
 }
 
 // Header bytes 0, 2, 3, 6 of a packet (payload_cksum), packed b0 | b2 << 8 |
@@ -658,8 +686,10 @@ k_cksum_flat(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
                                     len | (ph.hl << 16) | (ph.v4 << 24)};
         // Row marks carry the row's number within the tile; reset them to a
         // tag no row has so the previous tile's marks can't match.
-        L.mark[lane] = 0xFFFFFFFFu;
-        wave_sync_lds();
+#pragma unroll
+        for (int u = 0; u < UN; ++u)
+            L.mark[u][lane] = 0xFFFFFFFFu;
+        wave_order();
 
         uint32_t acc = ph.special;
         constexpr uint32_t kGrp = 64u * UN;
@@ -696,7 +726,7 @@ k_cksum_flat(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
         if constexpr (HDR)
             if (valid)
                 out_hdr[p] = ph.v4 ? lane_hdr_cksum<NT>(a, ph.hl, lut) : 0;
-        wave_sync_lds(); // the tables are rewritten by the next tile
+        wave_order(); // the tables are rewritten by the next tile
     }
     if (bad) {
 #pragma unroll
