@@ -225,63 +225,29 @@ __device__ __forceinline__ void accum_full(const u32x4 &d, uint32_t &E, uint32_t
     O = dot4(d.w, kOddW, O);
 }
 
-// Byte mask (0xFF per selected byte) of the bytes of dword j of a 16-byte
-// chunk that fall in [lo, hi), both relative to the chunk.
-__device__ __forceinline__ uint32_t dword_mask(int lo, int hi, int j)
-{
-    const int l = min(max(lo - 4 * j, 0), 4);
-    const int h = min(max(hi - 4 * j, 0), 4);
-    const uint64_t m = ((1ull << (8 * h)) - 1ull) & ~((1ull << (8 * l)) - 1ull);
-    return (uint32_t)m;
-}
-
-// accum_masked without tables (for the rare edge chunks of the strided
-// kernel): same weights, computed arithmetically.  With HDR, the bytes of the
-// IP header [0, hl) are also summed into (Eh, Oh) for the fused IPv4 header
-// checksum.
-template <int KIND, bool HDR>
-__device__ __forceinline__ void accum_edge(const u32x4 &d, int co, int rs, int re,
-                                           uint32_t v4, uint32_t &E, uint32_t &O,
-                                           uint32_t &Eh, uint32_t &Oh)
-{
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        uint32_t w = dword_mask(rs - co, re - co, j) & 0x01010101u;
-        if constexpr (KIND == WC_KIND_PAYLOAD) {
-            const uint32_t h = v4 ? (dword_mask(9 - co, 10 - co, j) |
-                                     dword_mask(12 - co, 20 - co, j))
-                                  : (dword_mask(4 - co, 6 - co, j) |
-                                     dword_mask(8 - co, 40 - co, j));
-            w += h & 0x01010101u;
-        }
-        const uint32_t x = pick_dword(d, j);
-        E = dot4(x, w & kEvenB, E);
-        O = dot4(x, w & kOddB, O);
-        if constexpr (HDR) {
-            const uint32_t m = dword_mask(-co, rs - co, j);
-            Eh = dot4(x, m & kEvenW, Eh);
-            Oh = dot4(x, m & kOddW, Oh);
-        }
-    }
-}
-
 // One chunk of the strided kernel: chunks strictly inside the summed range
-// (and past the header) take the full-weight path; the wave takes the edge
-// path only when one of its lanes holds a head / tail / header chunk.
+// (and past the header) take the full-weight path; the wave takes the table
+// path only when one of its lanes holds a head / tail / header chunk.  With
+// HDR the IP header bytes [0, hl) also go into (Eh, Oh) for the fused IPv4
+// header checksum.
 template <int KIND, bool FULL, bool HDR>
 __device__ __forceinline__ void accum_strided(const u32x4 &d, int co, int rs, int re,
-                                              uint32_t v4, uint32_t &E, uint32_t &O,
-                                              uint32_t &Eh, uint32_t &Oh)
+                                              uint32_t v4, const WeightLut &M,
+                                              uint32_t &E, uint32_t &O, uint32_t &Eh,
+                                              uint32_t &Oh)
 {
     if constexpr (FULL) {
         accum_full(d, E, O);
     } else {
         const int head = KIND == WC_KIND_PAYLOAD ? max(rs, 40) : rs;
         const bool edge = co < head || co + 16 > re;
-        if (__ballot(edge))
-            accum_edge<KIND, HDR>(d, co, rs, re, v4, E, O, Eh, Oh);
-        else
+        if (__ballot(edge)) {
+            accum_masked<KIND>(d, co, rs, re, v4, M, E, O);
+            if constexpr (HDR)
+                accum_masked<WC_KIND_IP>(d, co, 0, rs, 0u, M, Eh, Oh);
+        } else {
             accum_full(d, E, O);
+        }
     }
 }
 
@@ -320,6 +286,13 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
     constexpr int GPW = 64 / G;
     constexpr uint64_t PPW = (uint64_t)GPW * U;
     constexpr int PASS = G * CPL;
+
+    // Byte-weight tables for the edge chunks (not needed when FULL).
+    __shared__ WeightLut lut;
+    if constexpr (!FULL) {
+        load_weight_lut(lut);
+        __syncthreads();
+    }
 
     const int lane = threadIdx.x & 63;
     const int gl = lane & (G - 1);
@@ -379,7 +352,7 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
 #pragma unroll
             for (int c = 0; c < CPL; ++c)
                 accum_strided<KIND, FULL, HDR>(d[u][c], 16 * (gl + c * G) - s[u], rs, re,
-                                               ph.v4, E, O, Eh, Oh);
+                                               ph.v4, lut, E, O, Eh, Oh);
             // Packets longer than one pass (e.g. 9000 B jumbo frames).
             for (uint32_t kb = PASS; kb < nch[u]; kb += PASS) {
                 u32x4 t[CPL];
@@ -392,7 +365,7 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
 #pragma unroll
                 for (int c = 0; c < CPL; ++c)
                     accum_strided<KIND, FULL, HDR>(t[c], 16 * (int)(kb + gl + c * G) - s[u],
-                                                   rs, re, ph.v4, E, O, Eh, Oh);
+                                                   rs, re, ph.v4, lut, E, O, Eh, Oh);
             }
 
             uint32_t S = combine(E, O, s[u] & 1);
