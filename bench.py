@@ -53,6 +53,9 @@ def parse():
     ap.add_argument("--window-packets", type=int, default=1 << 25, help="c5 resident window")
     ap.add_argument("--packets", type=int, default=1 << 20)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--warmup-seconds", type=float, default=0.3,
+                    help="keep warming up (untimed) until this long has passed, so the "
+                         "GPU clock has ramped from idle before the timed steps")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-file", default=str(ROOT / "profiles" / "traffic.json"))
     return ap.parse_args()
@@ -146,7 +149,7 @@ def make_workload(args, dev, rank, world):
     meta = {"packets_per_gpu": n, "mean_packet_bytes": round(nbytes / n, 2),
             "layout": "ragged", "kind": kind}
     plan = {"kernel": "flat (chunk-balanced, 64-packet tiles)",
-            "rows_in_flight": int(os.environ.get("WC_FLAT_UN", "1")),
+            "rows_per_group": int(os.environ.get("WC_FLAT_UN", "2")),
             "grid": int((n + 255) // 256)}
     return step, n, nbytes, buf, out, plan, desc, meta, (offs, lens), "weak"
 
@@ -231,8 +234,13 @@ def main():
     step, n, nbytes, buf, out, plan, desc, meta, shape, scaling = make_workload(
         args, dev, rank, world)
 
-    for _ in range(args.warmup):
+    t_w = time.perf_counter()
+    done = 0
+    while done < args.warmup or time.perf_counter() - t_w < args.warmup_seconds:
         step()
+        done += 1
+        if done % 16 == 0:
+            torch.cuda.synchronize(dev)
     wdist.barrier(dev)
 
     stream = torch.cuda.current_stream(dev)  # the stream every launch goes to

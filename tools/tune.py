@@ -63,6 +63,7 @@ def main():
     ap.add_argument("--variants", default="")
     ap.add_argument("--ceiling", action="store_true")
     ap.add_argument("--json", default="")
+    ap.add_argument("--verbose", action="store_true", help="print every round's time")
     ap.add_argument("--kind", default="ip", choices=["ip", "payload"])
     ap.add_argument("--offset", type=int, default=0, help="byte offset of packet 0 (c2/c3)")
     ap.add_argument("--stride", type=int, default=0, help="packet stride (c2/c3; default len)")
@@ -143,6 +144,8 @@ def main():
                 fn()
                 ms = time_it(fn, args.iters, stream)
             times[name].append(ms)
+            if args.verbose:
+                print(f"  round {r} {name or 'default':<40} {ms * 1e3:9.1f} us", flush=True)
     apply("")
     rows = []
     for name, ts in times.items():
