@@ -99,7 +99,7 @@ def main():
             d_len = torch.full((n,), L, dtype=torch.int16, device=dev)
             run = lambda: wc.cksum_ragged(buf, d_off, d_len, out=out, kind=args.kind)  # noqa: E731
 
-    variants = [v.strip() for v in args.variants.split(";") if v.strip()] or [""]
+    variants = [("" if v.strip() == "default" else v.strip()) for v in args.variants.split(";") if v.strip()] or [""]
     base_env = {k: os.environ.get(k) for k in ("WC_SHAPE", "WC_NT", "WC_BLOCKS_PER_CU", "WC_GRID",
                                                 "WC_FLAT_UN", "WC_FLAT_TPW", "WC_DIAG_NOLOAD")}
 
