@@ -92,11 +92,16 @@ int wc_cksum_ip_udp_ragged(const void *d_base, const uint64_t *d_off,
 
 /* --- host-memory batch (end-to-end: pinned H2D, kernel, D2H) ------------- */
 
-/* Same as wc_cksum_ragged, but every buffer is host memory: the packet bytes
- * [h_base, h_base + h_bytes) are streamed to the GPU in chunks over several
- * HIP streams with hipMemcpyAsync, and the results come back into h_out.
- * Synchronous.  Register the buffer first (wc_host_register) to avoid an
- * extra host copy into the library's pinned staging ring. */
+/* Same as wc_cksum_ragged, but every buffer is host memory: packet i is
+ * h_len[i] bytes at h_base + h_off[i], inside [h_base, h_base + h_bytes)
+ * (WC_EINVAL otherwise), in any order.  Synchronous; results land in h_out.
+ *   - Registered region (wc_host_register), small batch (<= 4096 packets,
+ *     <= 8 MiB; WC_ZC_BYTES overrides): one kernel reads the packets in
+ *     place over PCIe -- the low-latency path for a socket or ring batch.
+ *   - Otherwise chunks are streamed over several HIP streams with
+ *     hipMemcpyAsync: ascending offsets ship the byte range a chunk covers
+ *     (DMA straight from a registered region), any other order is gathered
+ *     into the library's pinned staging first. */
 int wc_cksum_host(const void *h_base, uint64_t h_bytes, const uint64_t *h_off,
                   const uint16_t *h_len, uint64_t n, uint16_t *h_out, int kind);
 

@@ -102,6 +102,32 @@ def test_ragged_random_placement(gpu):
     np.testing.assert_array_equal(got, c_oracle.cksum_ragged(buf, offs, lens, kind=0))
 
 
+@pytest.mark.parametrize("shape", ["64,2,1", "64,4,1", "32,2,1", "16,2,2"])
+def test_ragged_group_kernel(gpu, monkeypatch, shape):
+    """The small-batch ragged group kernel (forced for every batch size):
+    golden vectors of both kinds, random overlapping placements with jumbo
+    and empty packets, and wild IPv4/IPv6 packets at odd alignment."""
+    monkeypatch.setenv("WC_FLAT_MIN", str(1 << 40))
+    monkeypatch.setenv("WC_RAGGED_SHAPE", shape)
+    g = np.load(GOLDEN / "vectors.npz")
+    for k, pre in ((0, "ip"), (1, "pl")):
+        out = wc.cksum_ragged(dev_u8(g[pre + "_blob"], gpu), to_dev(g[pre + "_off"], gpu),
+                              to_dev(g[pre + "_len"], gpu), kind=k)
+        np.testing.assert_array_equal(host(out), g[pre + "_expect"])
+    rng = np.random.default_rng(21)
+    buf = rng.integers(0, 256, 1 << 20, dtype=np.uint8)
+    lens = rng.integers(0, 9001, 5000).astype(np.uint16)
+    lens[:50] = 0
+    offs = rng.integers(0, buf.size - 9001, lens.size).astype(np.uint64)
+    got = host(wc.cksum_ragged(dev_u8(buf, gpu), to_dev(offs, gpu), to_dev(lens, gpu)))
+    np.testing.assert_array_equal(got, c_oracle.cksum_ragged(buf, offs, lens, kind=0))
+    pkts = random_packets(rng, 2000, max_payload=1472, wild=True)
+    buf, offs, lens = pack(pkts, align=1, lead=5)
+    got = host(wc.cksum_ragged(dev_u8(buf, gpu), to_dev(offs, gpu), to_dev(lens, gpu),
+                               kind="payload"))
+    np.testing.assert_array_equal(got, c_oracle.cksum_ragged(buf, offs, lens, kind=1))
+
+
 def test_all_zero_and_all_ones(gpu):
     for fill, want in ((0x00, 0xFFFF), (0xFF, 0x0000)):
         buf = np.full(1472 * 64, fill, dtype=np.uint8)
@@ -253,6 +279,57 @@ def test_host_path(gpu, register):
     np.testing.assert_array_equal(got, c_oracle.cksum_ragged(buf, offs, lens, kind=0))
 
 
+@pytest.mark.parametrize("kind", ["ip", "payload"])
+@pytest.mark.parametrize("n", [1, 64, 4096])
+def test_host_zero_copy_small_batches(gpu, kind, n):
+    """Registered pool, small batch, slots in pool order scrambled -- the
+    socket RX shape (backend_sock.c:145 pool, w_rx batches of 64)."""
+    rng = np.random.default_rng(n * 7 + len(kind))
+    slot = 2048
+    pool = np.zeros(4096 * slot, dtype=np.uint8)
+    pool[:] = rng.integers(0, 256, pool.size, dtype=np.uint8)
+    if kind == "payload":
+        pkts = random_packets(rng, n, max_payload=slot - 80, wild=True)
+        lens = np.array([ln for _, ln in pkts], dtype=np.uint16)
+    else:
+        lens = rng.integers(0, slot - 15, n).astype(np.uint16)
+        pkts = None
+    slots = rng.permutation(4096)[:n]
+    offs = (slots * slot + rng.integers(0, 16, n)).astype(np.uint64)
+    if pkts is not None:
+        for o, (p, _) in zip(offs, pkts):
+            pool[int(o): int(o) + len(p)] = np.frombuffer(p, dtype=np.uint8)
+    want = c_oracle.cksum_ragged(pool, offs, lens, kind=0 if kind == "ip" else 1)
+    wc.host_register(pool)
+    try:
+        got = wc.cksum_host(pool, offs, lens, kind=kind)
+    finally:
+        wc.host_unregister(pool)
+    np.testing.assert_array_equal(got, want)
+
+
+def test_host_path_unordered_gather(gpu):
+    """Offsets in random order through the pipelined path (gathered into
+    pinned staging), more than one 64 MiB chunk."""
+    rng = np.random.default_rng(13)
+    lens = synth.zipf_lengths(400000, seed=6)
+    offs = synth.packed_offsets(lens, lead=1)
+    buf = rng.integers(0, 256, int(offs[-1]) + int(lens[-1]) + 64, dtype=np.uint8)
+    perm = rng.permutation(lens.size)
+    offs, lens = offs[perm], lens[perm]
+    got = wc.cksum_host(buf, offs, lens, kind="ip")
+    np.testing.assert_array_equal(got, c_oracle.cksum_ragged(buf, offs, lens, kind=0))
+
+
+def test_host_path_rejects_out_of_range(gpu):
+    buf = np.zeros(4096, dtype=np.uint8)
+    with pytest.raises(wc.WcError):
+        wc.cksum_host(buf, np.array([4000], dtype=np.uint64), np.array([200], dtype=np.uint16))
+    with pytest.raises(wc.WcError):  # payload_cksum reads >= 20 header bytes
+        wc.cksum_host(buf, np.array([4090], dtype=np.uint64), np.array([4], dtype=np.uint16),
+                      kind="payload")
+
+
 def test_c_dropin_program(gpu, tmp_path):
     """A C caller linking libwccksum.so in place of in_cksum.c."""
     exe = tmp_path / "dropin"
@@ -264,6 +341,30 @@ def test_c_dropin_program(gpu, tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "dropin: ok" in r.stdout
+
+
+def build_sock_verify(out: Path) -> Path:
+    subprocess.run(["gcc", "-O2", "-std=gnu11", "-D__HIP_PLATFORM_AMD__",
+                    "-I/opt/rocm/include", f"-I{ROOT / 'include'}", f"-I{ROOT / 'oracle'}",
+                    str(ROOT / "tests" / "c" / "sock_verify.c"), str(ROOT / "oracle" / "wc_oracle.c"),
+                    "-o", str(out), f"-L{ROOT / 'warpcore_amd'}", "-lwccksum",
+                    "-L/opt/rocm/lib", "-lamdhip64", "-lpthread",
+                    f"-Wl,-rpath,{ROOT / 'warpcore_amd'}"], check=True)
+    return out
+
+
+@pytest.mark.parametrize("batch,length", [(1, 1472), (64, 1472), (7, 1)])
+def test_socket_rx_verify_pass(gpu, tmp_path, batch, length):
+    """SURVEY config 1 with the verify pass on the socket RX path (8(f) row
+    4): echo over loopback, every received payload checksummed by the GPU in
+    place from the registered pool and matched against TX and the oracle."""
+    exe = build_sock_verify(tmp_path / "sock_verify")
+    r = subprocess.run([str(exe), "-s", str(length), "-b", str(batch), "-l", "200"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["gpu_mismatch"] == 0 and res["oracle_mismatch"] == 0
+    assert res["packets_verified"] >= 50 * batch
 
 
 # ---------------------------------------------------------------------------

@@ -101,7 +101,8 @@ def main():
 
     variants = [("" if v.strip() == "default" else v.strip()) for v in args.variants.split(";") if v.strip()] or [""]
     base_env = {k: os.environ.get(k) for k in ("WC_SHAPE", "WC_NT", "WC_BLOCKS_PER_CU", "WC_GRID",
-                                                "WC_FLAT_UN", "WC_FLAT_TPW", "WC_DIAG_NOLOAD")}
+                                                "WC_FLAT_UN", "WC_FLAT_TPW", "WC_DIAG_NOLOAD",
+                                                "WC_FLAT_MIN", "WC_RAGGED_SHAPE")}
 
     def apply(spec):
         for k, v in base_env.items():

@@ -186,7 +186,10 @@ def cksum_ip_udp_ragged(base: torch.Tensor, offsets: torch.Tensor, lengths: torc
 
 def cksum_host(buf: np.ndarray, offsets: np.ndarray, lengths: np.ndarray,
                kind="ip") -> np.ndarray:
-    """Checksum host-resident packets: pinned H2D, kernel, D2H (synchronous)."""
+    """Checksum host-resident packets (synchronous), offsets in any order.
+
+    Small batches in a registered buffer are read in place by one kernel;
+    larger ones are streamed over pinned H2D copies (wc_cksum_host)."""
     buf = np.ascontiguousarray(buf).reshape(-1).view(np.uint8)
     off = np.ascontiguousarray(offsets, dtype=np.uint64)
     lens = np.ascontiguousarray(lengths, dtype=np.uint16)

@@ -29,6 +29,18 @@ constexpr int kPipe = 3;                          // host-path pipeline depth
 constexpr uint64_t kChunkBytes = 64ull << 20;     // host-path bytes per chunk
 constexpr uint64_t kChunkPkts = 1ull << 20;       // host-path packets per chunk
 constexpr uint64_t kScalarStage = 65536 + 64;     // one max-size packet
+constexpr uint64_t kZcPkts = 4096;                // zero-copy path: max packets
+constexpr int kFlatMinDefault = 0;                // ragged: flat kernel from n >= this
+
+// Small batches over registered memory skip the copy engines: the kernel
+// reads the packets straight out of the page-locked region over PCIe, and
+// the offsets, lengths and results sit in mapped pinned memory.  Batches up
+// to this many payload bytes take it (WC_ZC_BYTES overrides; 0 disables).
+constexpr int kZcBytesDefault = 8 << 20;
+// Zero-copy batches up to this many packets use the ragged group kernel
+// (every packet's loads cross PCIe at once); larger ones the flat kernel.
+// Measured on MI355X, tools/host_latency.py.
+constexpr uint64_t kZcGroupMax = 1024;
 
 struct HostPipe {
     hipStream_t st[kPipe] = {};
@@ -44,6 +56,14 @@ struct HostPipe {
     bool ready = false;
 };
 
+struct ZeroCopy {
+    hipStream_t st = nullptr;
+    uint64_t *h_off = nullptr, *d_off = nullptr; // mapped pinned
+    uint16_t *h_len = nullptr, *d_len = nullptr;
+    uint16_t *h_out = nullptr, *d_out = nullptr;
+    bool ready = false;
+};
+
 struct Device {
     bool ok = false;
     int cus = 0;
@@ -53,11 +73,17 @@ struct Device {
     uint16_t *h_res = nullptr;
     uint16_t *d_res = nullptr;
     HostPipe pipe;
+    ZeroCopy zc;
+};
+
+struct Registration {
+    uint64_t bytes;
+    const uint8_t *dptr; // device address of the region's first byte
 };
 
 std::mutex g_mu;
 Device g_dev[kMaxDevices];
-std::map<uintptr_t, uint64_t> g_registered; // host base -> bytes
+std::map<uintptr_t, Registration> g_registered; // host base -> region
 
 int hip_err(hipError_t e) { return e == hipSuccess ? WC_OK : -(int)e; }
 
@@ -163,17 +189,13 @@ wc::Shape shape_for_chunks(uint32_t nch)
     return {64, 9, 1};
 }
 
-bool shape_override(wc::Shape *sh)
+
+bool parse_shape(const char *v, wc::Shape *sh)
 {
-    const char *v = getenv("WC_SHAPE");
-    if (!v || !*v)
-        return false;
     int g = 0, c = 0, u = 0;
-    if (sscanf(v, "%d,%d,%d", &g, &c, &u) != 3)
+    if (!v || !*v || sscanf(v, "%d,%d,%d", &g, &c, &u) != 3)
         return false;
-    sh->group = g;
-    sh->cpl = c;
-    sh->unroll = u;
+    *sh = {g, c, u};
     return true;
 }
 
@@ -211,22 +233,36 @@ Plan plan_strided(const Device &D, uint64_t base, uint64_t stride, uint32_t len,
     const uint32_t phase = (stride % 16 == 0) ? (uint32_t)(base % 16) : 15u;
     const uint32_t nch = (phase + span + 15u) / 16u;
     p.shape = shape_for_chunks(nch);
-    shape_override(&p.shape);
+    parse_shape(getenv("WC_SHAPE"), &p.shape);
     p.full = kind == WC_CKSUM_IP && base % 16 == 0 && stride % 16 == 0 &&
              len % 16 == 0;
     p.grid = grid_for(D, p.shape, n);
     return p;
 }
 
-Plan plan_ragged(const Device &D, uint64_t n)
+// Ragged batches take the chunk-balanced flat kernel (group = 0 marks it;
+// unroll = 64-chunk rows per ping-pong group, WC_FLAT_UN).  A host
+// zero-copy batch of at most kZcGroupMax packets takes the ragged group
+// kernel instead: a flat wave walks its 64-packet tile's rows one PCIe
+// latency at a time, the group kernel issues every packet's loads at once.
+// (Device-resident batches measured no better on the group kernel at any
+// size -- launch cost dominates small ones -- so WC_FLAT_MIN defaults to 0.)
+// The fused header pass (out_hdr) exists in the flat kernel only.
+Plan plan_ragged(const Device &D, uint64_t n, bool zero_copy = false, bool hdr = false)
 {
     (void)D;
-    (void)n;
     Plan p;
-    // The chunk-balanced flat kernel (group = 0 marks it; unroll = 64-chunk
-    // rows per ping-pong group, WC_FLAT_UN overrides).
-    p.shape = {0, 1, env_int("WC_FLAT_UN", 2)};
     p.full = false;
+    const bool small = (zero_copy && n <= kZcGroupMax) ||
+                       n < (uint64_t)env_int("WC_FLAT_MIN", kFlatMinDefault);
+    if (small && !hdr) {
+        p.shape = {64, 2, 1};
+        parse_shape(getenv("WC_RAGGED_SHAPE"), &p.shape);
+        const uint64_t ppw = (uint64_t)(64 / p.shape.group) * p.shape.unroll;
+        p.grid = (int)std::max<uint64_t>(1, ((n + ppw - 1) / ppw + 3) / 4);
+        return p;
+    }
+    p.shape = {0, 1, env_int("WC_FLAT_UN", 2)};
     p.grid = 0;
     return p;
 }
@@ -277,7 +313,7 @@ int batch_ragged(const void *d_base, const uint64_t *d_off, const uint16_t *d_le
     int rc = ensure_device(&D);
     if (rc)
         return rc;
-    const Plan p = plan_ragged(*D, n);
+    const Plan p = plan_ragged(*D, n, false, d_out_hdr != nullptr);
     wc::LaunchArgs a{d_base, 0,     0,    d_off, d_len, n,
                      d_out,  d_bad, kind, true,  false, nontemporal(), flat_tpw(),
                      d_out_hdr, env_int("WC_DIAG_NOLOAD", 0) != 0};
@@ -341,14 +377,169 @@ int pipe_init_locked(Device &D)
     return WC_OK;
 }
 
-bool is_registered_locked(const void *p, uint64_t bytes)
+int zc_init_locked(Device &D)
+{
+    ZeroCopy &Z = D.zc;
+    if (Z.ready)
+        return WC_OK;
+    const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
+    if (hipStreamCreateWithFlags(&Z.st, hipStreamNonBlocking) != hipSuccess ||
+        hipHostMalloc((void **)&Z.h_off, kZcPkts * 8, fl) != hipSuccess ||
+        hipHostMalloc((void **)&Z.h_len, kZcPkts * 2, fl) != hipSuccess ||
+        hipHostMalloc((void **)&Z.h_out, kZcPkts * 2, fl) != hipSuccess ||
+        hipHostGetDevicePointer((void **)&Z.d_off, Z.h_off, 0) != hipSuccess ||
+        hipHostGetDevicePointer((void **)&Z.d_len, Z.h_len, 0) != hipSuccess ||
+        hipHostGetDevicePointer((void **)&Z.d_out, Z.h_out, 0) != hipSuccess)
+        return WC_ENOMEM;
+    Z.ready = true;
+    return WC_OK;
+}
+
+// Device address of host range [p, p + bytes) if it lies inside one
+// registered region, else nullptr.
+const uint8_t *registered_dptr_locked(const void *p, uint64_t bytes)
 {
     const uintptr_t a = (uintptr_t)p;
     auto it = g_registered.upper_bound(a);
     if (it == g_registered.begin())
-        return false;
+        return nullptr;
     --it;
-    return a >= it->first && a + bytes <= it->first + it->second;
+    if (a < it->first || a + bytes > it->first + it->second.bytes)
+        return nullptr;
+    return it->second.dptr + (a - it->first);
+}
+
+// Bytes the reference reads for one packet (payload_cksum reads the IPv4
+// header fields up to byte 19 whatever len is, in_cksum.c:149-151).
+uint64_t span_of(uint16_t len, int kind)
+{
+    return kind == WC_CKSUM_PAYLOAD ? std::max<uint64_t>(len, 20) : len;
+}
+
+int zc_bytes() { return env_int("WC_ZC_BYTES", kZcBytesDefault); }
+
+// Small registered batch: one launch reading host memory in place.
+int host_zero_copy(Device &D, const uint8_t *dbase, const uint64_t *h_off,
+                   const uint16_t *h_len, uint64_t n, uint16_t *h_out, int kind)
+{
+    int rc = zc_init_locked(D);
+    if (rc)
+        return rc;
+    ZeroCopy &Z = D.zc;
+    memcpy(Z.h_off, h_off, n * 8);
+    memcpy(Z.h_len, h_len, n * 2);
+    const Plan p = plan_ragged(D, n, true);
+    wc::LaunchArgs a{dbase, 0,       0,    Z.d_off, Z.d_len, n,
+                     Z.d_out, nullptr, kind, true,    false,   nontemporal(),
+                     flat_tpw()};
+    rc = run(D, a, p, Z.st);
+    if (rc)
+        return rc;
+    hipError_t e = hipStreamSynchronize(Z.st);
+    if (e != hipSuccess)
+        return hip_err(e);
+    memcpy(h_out, (const void *)Z.h_out, n * 2);
+    return WC_OK;
+}
+
+// Pipelined path: chunks of packets go through kPipe streams, each chunk
+// H2D -> kernel -> D2H.  An ascending batch ships the byte range its chunk
+// covers (straight from registered memory, else via pinned staging); any
+// other order is gathered packet by packet into pinned staging first.
+int host_pipeline(Device &D, const uint8_t *hb, bool registered, bool ascending,
+                  const uint64_t *h_off, const uint16_t *h_len, uint64_t n,
+                  uint16_t *h_out, int kind)
+{
+    HostPipe &P = D.pipe;
+    uint64_t pend_lo[kPipe] = {}, pend_n[kPipe] = {};
+    bool pend[kPipe] = {};
+    auto drain = [&](int s) -> int {
+        if (!pend[s])
+            return WC_OK;
+        hipError_t e = hipEventSynchronize(P.done[s]);
+        if (e != hipSuccess)
+            return hip_err(e);
+        memcpy(h_out + pend_lo[s], P.h_out[s], pend_n[s] * 2);
+        pend[s] = false;
+        return WC_OK;
+    };
+
+    uint64_t i = 0;
+    int slot = 0;
+    while (i < n) {
+        int rc = drain(slot);
+        if (rc)
+            return rc;
+        uint64_t j = i, bytes = 0;
+        const uint8_t *src = nullptr;
+        if (ascending) {
+            const uint64_t lo = h_off[i];
+            uint64_t hi = lo;
+            while (j < n && j - i < kChunkPkts) {
+                const uint64_t e = h_off[j] + span_of(h_len[j], kind);
+                if (std::max(hi, e) - lo > kChunkBytes && j > i)
+                    break;
+                hi = std::max(hi, e);
+                P.h_off[slot][j - i] = h_off[j] - lo;
+                P.h_len[slot][j - i] = h_len[j];
+                ++j;
+            }
+            bytes = hi - lo;
+            src = hb + lo;
+            if (!registered) {
+                memcpy(P.h_bytes[slot], src, bytes);
+                src = P.h_bytes[slot];
+            }
+        } else {
+            while (j < n && j - i < kChunkPkts) {
+                const uint64_t sp = span_of(h_len[j], kind);
+                if (bytes + sp > kChunkBytes && j > i)
+                    break;
+                memcpy(P.h_bytes[slot] + bytes, hb + h_off[j], sp);
+                P.h_off[slot][j - i] = bytes;
+                P.h_len[slot][j - i] = h_len[j];
+                bytes += sp;
+                ++j;
+            }
+            src = P.h_bytes[slot];
+        }
+        const uint64_t cnt = j - i;
+        hipStream_t st = P.st[slot];
+        hipError_t e = hipMemcpyAsync(P.d_bytes[slot], src, bytes,
+                                      hipMemcpyHostToDevice, st);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(P.d_off[slot], P.h_off[slot], cnt * 8,
+                               hipMemcpyHostToDevice, st);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(P.d_len[slot], P.h_len[slot], cnt * 2,
+                               hipMemcpyHostToDevice, st);
+        if (e != hipSuccess)
+            return hip_err(e);
+        const Plan p = plan_ragged(D, cnt);
+        wc::LaunchArgs a{P.d_bytes[slot], 0,    0,    P.d_off[slot], P.d_len[slot],
+                         cnt,             P.d_out[slot], nullptr, kind, true,
+                         false,           nontemporal(), flat_tpw()};
+        rc = run(D, a, p, st);
+        if (rc)
+            return rc;
+        e = hipMemcpyAsync(P.h_out[slot], P.d_out[slot], cnt * 2,
+                           hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess)
+            e = hipEventRecord(P.done[slot], st);
+        if (e != hipSuccess)
+            return hip_err(e);
+        pend[slot] = true;
+        pend_lo[slot] = i;
+        pend_n[slot] = cnt;
+        i = j;
+        slot = (slot + 1) % kPipe;
+    }
+    for (int s = 0; s < kPipe; ++s) {
+        int rc = drain((slot + s) % kPipe);
+        if (rc)
+            return rc;
+    }
+    return WC_OK;
 }
 
 } // namespace
@@ -432,10 +623,16 @@ int wc_host_register(void *h_ptr, uint64_t bytes)
     int rc = init_locked(-1, &D);
     if (rc)
         return rc;
-    hipError_t e = hipHostRegister(h_ptr, bytes, hipHostRegisterDefault);
+    hipError_t e = hipHostRegister(h_ptr, bytes, hipHostRegisterMapped);
     if (e != hipSuccess)
         return hip_err(e);
-    g_registered[(uintptr_t)h_ptr] = bytes;
+    void *dptr = nullptr;
+    e = hipHostGetDevicePointer(&dptr, h_ptr, 0);
+    if (e != hipSuccess) {
+        (void)hipHostUnregister(h_ptr);
+        return hip_err(e);
+    }
+    g_registered[(uintptr_t)h_ptr] = Registration{bytes, (const uint8_t *)dptr};
     return WC_OK;
 }
 
@@ -461,105 +658,31 @@ int wc_cksum_host(const void *h_base, uint64_t h_bytes, const uint64_t *h_off,
     if (!h_base || !h_off || !h_len || !h_out)
         return WC_EINVAL;
 
+    // Every packet must lie inside the region; note the order and the bytes.
+    bool ascending = true;
+    uint64_t total = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t o = h_off[i];
+        const uint64_t sp = span_of(h_len[i], kind);
+        if (o > h_bytes || sp > h_bytes - o)
+            return WC_EINVAL;
+        ascending &= i == 0 || o >= h_off[i - 1];
+        total += sp;
+    }
+
     std::lock_guard<std::mutex> lk(g_mu);
     Device *D = nullptr;
     int rc = init_locked(-1, &D);
     if (rc)
         return rc;
+    const uint8_t *dbase = registered_dptr_locked(h_base, h_bytes);
+    if (dbase && n <= kZcPkts && total <= (uint64_t)zc_bytes())
+        return host_zero_copy(*D, dbase, h_off, h_len, n, h_out, kind);
     rc = pipe_init_locked(*D);
     if (rc)
         return rc;
-    HostPipe &P = D->pipe;
-    const bool direct = is_registered_locked(h_base, h_bytes);
-    const uint8_t *hb = (const uint8_t *)h_base;
-
-    // Bytes each packet needs (payload_cksum reads >= 20 header bytes).
-    auto span_of = [kind](uint16_t l) -> uint64_t {
-        return kind == WC_CKSUM_PAYLOAD ? std::max<uint64_t>(l, 20) : l;
-    };
-
-    // Pipeline over chunks of packets listed in ascending address order; a
-    // chunk is the byte range its packets cover.
-    uint64_t i = 0;
-    int slot = 0;
-    uint64_t pend_lo[kPipe] = {}, pend_n[kPipe] = {};
-    bool pend[kPipe] = {};
-    auto drain = [&](int s) -> int {
-        if (!pend[s])
-            return WC_OK;
-        hipError_t e = hipEventSynchronize(P.done[s]);
-        if (e != hipSuccess)
-            return hip_err(e);
-        memcpy(h_out + pend_lo[s], P.h_out[s], pend_n[s] * 2);
-        pend[s] = false;
-        return WC_OK;
-    };
-
-    while (i < n) {
-        rc = drain(slot);
-        if (rc)
-            return rc;
-        const uint64_t lo = h_off[i];
-        uint64_t hi = lo, j = i;
-        while (j < n && j - i < kChunkPkts) {
-            const uint64_t o = h_off[j];
-            const uint64_t e = o + span_of(h_len[j]);
-            if (o < lo || e > h_bytes) // descending order or out of range
-                return WC_EINVAL;
-            if (std::max(hi, e) - lo > kChunkBytes) {
-                if (j == i)
-                    return WC_EINVAL;
-                break;
-            }
-            hi = std::max(hi, e);
-            ++j;
-        }
-        const uint64_t cnt = j - i, bytes = hi - lo;
-        for (uint64_t k = 0; k < cnt; ++k) {
-            P.h_off[slot][k] = h_off[i + k] - lo;
-            P.h_len[slot][k] = h_len[i + k];
-        }
-        hipStream_t st = P.st[slot];
-        const uint8_t *src = hb + lo;
-        if (!direct) {
-            memcpy(P.h_bytes[slot], src, bytes);
-            src = P.h_bytes[slot];
-        }
-        hipError_t e = hipMemcpyAsync(P.d_bytes[slot], src, bytes,
-                                      hipMemcpyHostToDevice, st);
-        if (e == hipSuccess)
-            e = hipMemcpyAsync(P.d_off[slot], P.h_off[slot], cnt * 8,
-                               hipMemcpyHostToDevice, st);
-        if (e == hipSuccess)
-            e = hipMemcpyAsync(P.d_len[slot], P.h_len[slot], cnt * 2,
-                               hipMemcpyHostToDevice, st);
-        if (e != hipSuccess)
-            return hip_err(e);
-        const Plan p = plan_ragged(*D, cnt);
-        wc::LaunchArgs a{P.d_bytes[slot], 0,    0,    P.d_off[slot], P.d_len[slot],
-                         cnt,             P.d_out[slot], nullptr, kind, true,
-                         false,           nontemporal(), flat_tpw()};
-        rc = run(*D, a, p, st);
-        if (rc)
-            return rc;
-        e = hipMemcpyAsync(P.h_out[slot], P.d_out[slot], cnt * 2,
-                           hipMemcpyDeviceToHost, st);
-        if (e == hipSuccess)
-            e = hipEventRecord(P.done[slot], st);
-        if (e != hipSuccess)
-            return hip_err(e);
-        pend[slot] = true;
-        pend_lo[slot] = i;
-        pend_n[slot] = cnt;
-        i = j;
-        slot = (slot + 1) % kPipe;
-    }
-    for (int s = 0; s < kPipe; ++s) {
-        rc = drain((slot + s) % kPipe);
-        if (rc)
-            return rc;
-    }
-    return WC_OK;
+    return host_pipeline(*D, (const uint8_t *)h_base, dbase != nullptr, ascending,
+                         h_off, h_len, n, h_out, kind);
 }
 
 int wc_gpu_init(int device)
@@ -591,6 +714,13 @@ int wc_gpu_fini(void)
                 (void)hipStreamDestroy(P.st[s]);
             }
             P = HostPipe{};
+        }
+        if (D.zc.ready) {
+            (void)hipStreamSynchronize(D.zc.st);
+            (void)hipStreamDestroy(D.zc.st);
+            (void)hipHostFree(D.zc.h_off);
+            (void)hipHostFree(D.zc.h_len);
+            (void)hipHostFree(D.zc.h_out);
         }
         (void)hipStreamSynchronize(D.scalar_st);
         (void)hipStreamDestroy(D.scalar_st);

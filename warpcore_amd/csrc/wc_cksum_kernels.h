@@ -31,6 +31,14 @@
     WC_SHAPE(64, 9, 1)                                                         \
     WC_SHAPE(64, 9, 2)
 
+// Shapes of the small-batch ragged group kernel (ip_cksum / payload_cksum,
+// nontemporal loads).
+#define WC_RAGGED_SHAPE_LIST                                                   \
+    WC_SHAPE(16, 2, 2)                                                         \
+    WC_SHAPE(32, 2, 1)                                                         \
+    WC_SHAPE(64, 2, 1)                                                         \
+    WC_SHAPE(64, 4, 1)
+
 namespace wc {
 
 struct LaunchArgs {
@@ -43,7 +51,7 @@ struct LaunchArgs {
     uint16_t *out;
     uint64_t *bad;
     int kind;
-    bool ragged; // informational: ragged batches always use the flat kernel
+    bool ragged; // offs/lens batch: flat kernel, or the ragged group kernel
     bool full;
     bool nontemporal;
     int tiles_per_wave; // flat kernel: 64-packet tiles each wave walks
@@ -57,6 +65,8 @@ struct Shape {
     int unroll; // packets per group per iteration
 };
 
+// Group-per-packet kernel: strided, or (a.ragged) the small-batch ragged
+// variant over WC_RAGGED_SHAPE_LIST.
 hipError_t launch_cksum(const LaunchArgs &a, const Shape &sh, int grid,
                         hipStream_t st);
 // Chunk-balanced kernel for ragged batches (rows = 64-chunk rows per

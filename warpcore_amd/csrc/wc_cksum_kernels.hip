@@ -272,14 +272,19 @@ __device__ __forceinline__ uint32_t group_sum(uint32_t v)
 //   NT    nontemporal loads
 //   HDR   (payload only) also store ip_cksum(ip, ip4_hl) of each IPv4 packet
 //         into out_hdr (0 for IPv6, which has no header checksum)
+//   RAGGED packet i is [base + offs[i], + lens[i]) instead: the small-batch
+//         ragged variant (a few packets per wave, so a batch far smaller than
+//         the GPU still puts every packet's loads in flight at once)
 // Packet i is [base + i*stride, + len).  The grid is one-shot by default
 // (each wave does one iteration); a capped grid strides.
-template <int G, int CPL, int U, int KIND, bool FULL, bool NT, bool HDR>
+template <int G, int CPL, int U, int KIND, bool FULL, bool NT, bool HDR, bool RAGGED>
 __global__ void __launch_bounds__(256)
 k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
+        const uint64_t *__restrict__ offs, const uint16_t *__restrict__ lens,
         uint64_t n, uint16_t *__restrict__ out, unsigned long long *__restrict__ bad,
         uint16_t *__restrict__ out_hdr)
 {
+    static_assert(!(RAGGED && (FULL || HDR)), "ragged group variant: masked, no header");
     static_assert(!HDR || KIND == WC_KIND_PAYLOAD, "header checksum rides on payload");
     static_assert(G >= 4 && G <= 64 && (G & (G - 1)) == 0, "group width");
     static_assert(!(FULL && KIND == WC_KIND_PAYLOAD), "payload needs masks");
@@ -300,14 +305,11 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
     const int lead = lane & ~(G - 1);
     const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    // payload_cksum reads the IPv4 header fields up to byte 19 even for a
-    // shorter len (in_cksum.c:149-151), so cover them too.
-    const uint32_t span = KIND == WC_KIND_PAYLOAD ? max(len, 20u) : len;
     uint32_t nbad = 0;
 
     for (uint64_t p0 = wave * PPW; p0 < n; p0 += nwaves * PPW) {
         uint64_t c0[U];
-        uint32_t nch[U];
+        uint32_t nch[U], plen[U];
         int s[U];
         bool valid[U];
         u32x4 d[U][CPL];
@@ -316,7 +318,18 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
         for (int u = 0; u < U; ++u) {
             const uint64_t i = p0 + (uint64_t)u * GPW + grp;
             valid[u] = i < n;
-            const uint64_t a = (uint64_t)base + (valid[u] ? i : p0) * stride;
+            const uint64_t ii = valid[u] ? i : p0;
+            uint64_t a;
+            if constexpr (RAGGED) {
+                a = (uint64_t)base + offs[ii];
+                plen[u] = lens[ii];
+            } else {
+                a = (uint64_t)base + ii * stride;
+                plen[u] = len;
+            }
+            // payload_cksum reads the IPv4 header fields up to byte 19 even
+            // for a shorter len (in_cksum.c:149-151), so cover them too.
+            const uint32_t span = KIND == WC_KIND_PAYLOAD ? max(plen[u], 20u) : plen[u];
             s[u] = (int)(a & 15u);
             c0[u] = a & ~15ull;
             nch[u] = valid[u] ? (uint32_t)((a + span + 15u - c0[u]) >> 4) : 0u;
@@ -346,7 +359,7 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
                                            lead + ((su + 6) >> 4), 64);
                 ph = pseudo_hdr(b0, b2, b3, b6);
             }
-            const int rs = (int)ph.hl, re = (int)len;
+            const int rs = (int)ph.hl, re = (int)plen[u];
 
             uint32_t E = 0, O = 0, Eh = 0, Oh = 0;
 #pragma unroll
@@ -747,12 +760,13 @@ k_synth(uint8_t *__restrict__ buf, uint64_t nbytes, uint64_t seed)
 // ---------------------------------------------------------------------------
 // Launch table.
 
-template <int G, int CPL, int U, int KIND, bool FULL, bool NT, bool HDR = false>
+template <int G, int CPL, int U, int KIND, bool FULL, bool NT, bool HDR = false,
+          bool RAGGED = false>
 static hipError_t launch_one(const LaunchArgs &a, int grid, hipStream_t st)
 {
-    hipLaunchKernelGGL((k_cksum<G, CPL, U, KIND, FULL, NT, HDR>), dim3(grid), dim3(256), 0,
-                       st, (const uint8_t *)a.base, a.stride, a.len, a.n, a.out,
-                       (unsigned long long *)a.bad, a.out_hdr);
+    hipLaunchKernelGGL((k_cksum<G, CPL, U, KIND, FULL, NT, HDR, RAGGED>), dim3(grid),
+                       dim3(256), 0, st, (const uint8_t *)a.base, a.stride, a.len, a.offs,
+                       a.lens, a.n, a.out, (unsigned long long *)a.bad, a.out_hdr);
     return hipGetLastError();
 }
 
@@ -773,8 +787,26 @@ static hipError_t launch_shape(const LaunchArgs &a, int grid, hipStream_t st)
               : launch_one<G, CPL, U, WC_KIND_IP, false, false>(a, grid, st);
 }
 
+template <int G, int CPL, int U>
+static hipError_t launch_ragged_shape(const LaunchArgs &a, int grid, hipStream_t st)
+{
+    if (a.kind == WC_KIND_PAYLOAD)
+        return launch_one<G, CPL, U, WC_KIND_PAYLOAD, false, true, false, true>(a, grid, st);
+    return launch_one<G, CPL, U, WC_KIND_IP, false, true, false, true>(a, grid, st);
+}
+
 hipError_t launch_cksum(const LaunchArgs &a, const Shape &sh, int grid, hipStream_t st)
 {
+    if (a.ragged) {
+        if (a.out_hdr)
+            return hipErrorInvalidValue;
+#define WC_SHAPE(G_, C_, U_)                                                   \
+    if (sh.group == G_ && sh.cpl == C_ && sh.unroll == U_)                     \
+        return launch_ragged_shape<G_, C_, U_>(a, grid, st);
+        WC_RAGGED_SHAPE_LIST
+#undef WC_SHAPE
+        return hipErrorInvalidValue;
+    }
 #define WC_SHAPE(G_, C_, U_)                                                   \
     if (sh.group == G_ && sh.cpl == C_ && sh.unroll == U_)                     \
         return launch_shape<G_, C_, U_>(a, grid, st);
