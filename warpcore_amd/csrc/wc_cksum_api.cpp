@@ -235,7 +235,7 @@ Plan plan_strided(const Device &D, uint64_t base, uint64_t stride, uint32_t len,
     p.shape = shape_for_chunks(nch);
     parse_shape(getenv("WC_SHAPE"), &p.shape);
     p.full = kind == WC_CKSUM_IP && base % 16 == 0 && stride % 16 == 0 &&
-             len % 16 == 0;
+             len % 16 == 0 && !(env_int("WC_VARIANT", 0) & 2);
     p.grid = grid_for(D, p.shape, n);
     return p;
 }
@@ -296,6 +296,7 @@ int batch_strided(const void *d_base, uint64_t stride, uint16_t len, uint64_t n,
     wc::LaunchArgs a{d_base, stride, len,  nullptr,  nullptr, n,
                      d_out,  d_bad,  kind, false,    p.full,  nontemporal(),
                      0,      d_out_hdr};
+    a.variant = env_int("WC_VARIANT", 0);
     return run(*D, a, p, (hipStream_t)stream);
 }
 
@@ -317,6 +318,7 @@ int batch_ragged(const void *d_base, const uint64_t *d_off, const uint16_t *d_le
     wc::LaunchArgs a{d_base, 0,     0,    d_off, d_len, n,
                      d_out,  d_bad, kind, true,  false, nontemporal(), flat_tpw(),
                      d_out_hdr, env_int("WC_DIAG_NOLOAD", 0) != 0};
+    a.variant = env_int("WC_VARIANT", 0);
     return run(*D, a, p, (hipStream_t)stream);
 }
 

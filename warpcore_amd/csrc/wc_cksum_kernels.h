@@ -57,6 +57,7 @@ struct LaunchArgs {
     int tiles_per_wave; // flat kernel: 64-packet tiles each wave walks
     uint16_t *out_hdr;  // payload kind: also the IPv4 header checksums (or null)
     bool diag_noload;   // WC_DIAG_NOLOAD=1: timing-only flat build (wrong results)
+    int variant = 0;    // WC_VARIANT: experimental kernel variants (A/B tuning)
 };
 
 struct Shape {

@@ -20,8 +20,9 @@
 //     O + 256*E (odd start), modulo 2^32 -- bit-identical for every alignment,
 //     including the reference's uint32 wrap on IPv6 next_hdr << 24
 //     (in_cksum.c:157).  Head/tail masking and the pseudo-header fields
-//     payload_cksum adds with their natural word weight are dot4 byte weights,
-//     looked up in small LDS tables.
+//     payload_cksum adds with their natural word weight are dot4 byte weights:
+//     computed from the range bounds in the strided kernel (edge chunks are
+//     rare there), looked up in small LDS tables in the flat kernel.
 //   * Strided batches: a GROUP of G lanes of one wave64 owns a packet (G = 64
 //     is "one packet per wavefront"), every lane issuing CPL x U loads before
 //     any arithmetic.  Ragged batches: the chunk-balanced flat kernel deals
@@ -164,8 +165,12 @@ constexpr WeightTable make_weight_table()
     return t;
 }
 
-// Generated at compile time; each block copies it into LDS (6.4 KB).
+// Generated at compile time; each flat-kernel block copies it into LDS (6.4 KB).
 __device__ const WeightTable kWeightTable = make_weight_table();
+
+// 16 zero bytes: the strided kernel's dead load slots read this instead of
+// branching around the load.
+__device__ __attribute__((aligned(16))) const uint32_t kZeroChunk[4] = {0u, 0u, 0u, 0u};
 
 __device__ __forceinline__ void load_weight_lut(WeightLut &M)
 {
@@ -225,26 +230,67 @@ __device__ __forceinline__ void accum_full(const u32x4 &d, uint32_t &E, uint32_t
     O = dot4(d.w, kOddW, O);
 }
 
+// Arithmetic byte weights (no tables): bit b of a 16-bit chunk mask becomes
+// weight 0x01 in byte b.  n * 0x204081 places bit k of a nibble at bits
+// k, k+7, k+14, k+21 -- all distinct, so no carries -- and bits 0/8/16/24
+// come from k = 0/1/2/3 alone.
+__device__ __forceinline__ uint32_t expand_nibble(uint32_t bits, int j)
+{
+    return (((bits >> (4 * j)) & 0xFu) * 0x00204081u) & 0x01010101u;
+}
+
+// Pseudo-header field bytes of payload_cksum as bit masks over packet offsets
+// (same fields as hdr_field above), pre-shifted by 16 so a chunk starting at
+// co >= -16 reads its 16 bits at (co + 16).
+constexpr uint64_t kHdrBitsV4 = ((1ull << 9) | (0xFFull << 12)) << 16;
+constexpr uint64_t kHdrBitsV6 = ((1ull << 4) | (1ull << 5) | (0xFFFFFFFFull << 8)) << 16;
+
+// accum_masked without the LDS tables: the weights are computed from the
+// range bounds, a few VALU ops per dword (used where edge chunks are rare).
+template <int KIND>
+__device__ __forceinline__ void accum_arith(const u32x4 &d, int co, int rs, int re,
+                                            uint32_t v4, uint32_t &E, uint32_t &O)
+{
+    const int lo = min(max(rs - co, 0), 16);
+    const int hi = max(min(max(re - co, 0), 16), lo);
+    const uint32_t kb = (1u << hi) - (1u << lo);
+    uint32_t hb = 0;
+    if constexpr (KIND == WC_KIND_PAYLOAD) {
+        const uint32_t sh = (uint32_t)min(co + 16, 63);
+        hb = (uint32_t)((v4 ? kHdrBitsV4 : kHdrBitsV6) >> sh) & 0xFFFFu;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        uint32_t w = expand_nibble(kb, j);
+        if constexpr (KIND == WC_KIND_PAYLOAD)
+            w += expand_nibble(hb, j); // byte weights <= 2
+        const uint32_t x = pick_dword(d, j);
+        E = dot4(x, w & kEvenB, E);
+        O = dot4(x, w & kOddB, O);
+    }
+}
+
 // One chunk of the strided kernel: chunks strictly inside the summed range
-// (and past the header) take the full-weight path; the wave takes the table
-// path only when one of its lanes holds a head / tail / header chunk.  With
-// HDR the IP header bytes [0, hl) also go into (Eh, Oh) for the fused IPv4
-// header checksum.
+// (and past the header) take the full-weight path; the wave takes the masked
+// path only when one of its lanes holds a head / tail / header chunk of its
+// packet (`live`: the chunk is one of the packet's own -- slots past the end
+// hold zeros and need no mask).  Edge weights are computed (accum_arith), so
+// the strided kernel needs no LDS at all.  With HDR the IP header bytes
+// [0, hl) also go into (Eh, Oh) for the fused IPv4 header checksum.
 template <int KIND, bool FULL, bool HDR>
 __device__ __forceinline__ void accum_strided(const u32x4 &d, int co, int rs, int re,
-                                              uint32_t v4, const WeightLut &M,
-                                              uint32_t &E, uint32_t &O, uint32_t &Eh,
-                                              uint32_t &Oh)
+                                              bool live, uint32_t v4, uint32_t &E,
+                                              uint32_t &O, uint32_t &Eh, uint32_t &Oh)
 {
     if constexpr (FULL) {
         accum_full(d, E, O);
     } else {
         const int head = KIND == WC_KIND_PAYLOAD ? max(rs, 40) : rs;
-        const bool edge = co < head || co + 16 > re;
+        const bool edge = live && (co < head || co + 16 > re);
         if (__ballot(edge)) {
-            accum_masked<KIND>(d, co, rs, re, v4, M, E, O);
+            accum_arith<KIND>(d, co, rs, re, v4, E, O);
             if constexpr (HDR)
-                accum_masked<WC_KIND_IP>(d, co, 0, rs, 0u, M, Eh, Oh);
+                accum_arith<WC_KIND_IP>(d, co, 0, rs, 0u, Eh, Oh);
         } else {
             accum_full(d, E, O);
         }
@@ -276,9 +322,12 @@ __device__ __forceinline__ uint32_t group_sum(uint32_t v)
 //         ragged variant (a few packets per wave, so a batch far smaller than
 //         the GPU still puts every packet's loads in flight at once)
 // Packet i is [base + i*stride, + len).  The grid is one-shot by default
-// (each wave does one iteration); a capped grid strides.
+// (each wave does one iteration); a capped grid strides.  waves_per_eu(3)
+// caps the kernel at 168 VGPRs: payload (16,6,4) otherwise takes 170, which
+// leaves 2 waves per SIMD and cost 10 % of HBM throughput (80 -> 88 % of peak,
+// profiles/ab_r01_c2_payload_waves.log).
 template <int G, int CPL, int U, int KIND, bool FULL, bool NT, bool HDR, bool RAGGED>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
 k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
         const uint64_t *__restrict__ offs, const uint16_t *__restrict__ lens,
         uint64_t n, uint16_t *__restrict__ out, unsigned long long *__restrict__ bad,
@@ -292,13 +341,6 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
     constexpr uint64_t PPW = (uint64_t)GPW * U;
     constexpr int PASS = G * CPL;
 
-    // Byte-weight tables for the edge chunks (not needed when FULL).
-    __shared__ WeightLut lut;
-    if constexpr (!FULL) {
-        load_weight_lut(lut);
-        __syncthreads();
-    }
-
     const int lane = threadIdx.x & 63;
     const int gl = lane & (G - 1);
     const int grp = lane / G;
@@ -306,6 +348,7 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
     const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     uint32_t nbad = 0;
+    const uint64_t zero = (uint64_t)(uintptr_t)&kZeroChunk;
 
     for (uint64_t p0 = wave * PPW; p0 < n; p0 += nwaves * PPW) {
         uint64_t c0[U];
@@ -339,8 +382,9 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
 #pragma unroll
             for (int c = 0; c < CPL; ++c) {
                 const uint32_t k = (uint32_t)(gl + c * G);
-                d[u][c] = k < nch[u] ? load_chunk<NT>(c0[u] + 16ull * k)
-                                     : u32x4{0u, 0u, 0u, 0u};
+                // Unconditional load (no branch per chunk): dead slots read a
+                // zero chunk.
+                d[u][c] = load_chunk<NT>(k < nch[u] ? c0[u] + 16ull * k : zero);
             }
 
 #pragma unroll
@@ -365,20 +409,21 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
 #pragma unroll
             for (int c = 0; c < CPL; ++c)
                 accum_strided<KIND, FULL, HDR>(d[u][c], 16 * (gl + c * G) - s[u], rs, re,
-                                               ph.v4, lut, E, O, Eh, Oh);
+                                               (uint32_t)(gl + c * G) < nch[u], ph.v4, E, O,
+                                               Eh, Oh);
             // Packets longer than one pass (e.g. 9000 B jumbo frames).
             for (uint32_t kb = PASS; kb < nch[u]; kb += PASS) {
                 u32x4 t[CPL];
 #pragma unroll
                 for (int c = 0; c < CPL; ++c) {
                     const uint32_t k = kb + (uint32_t)(gl + c * G);
-                    t[c] = k < nch[u] ? load_chunk<NT>(c0[u] + 16ull * k)
-                                      : u32x4{0u, 0u, 0u, 0u};
+                    t[c] = load_chunk<NT>(k < nch[u] ? c0[u] + 16ull * k : zero);
                 }
 #pragma unroll
                 for (int c = 0; c < CPL; ++c)
                     accum_strided<KIND, FULL, HDR>(t[c], 16 * (int)(kb + gl + c * G) - s[u],
-                                                   rs, re, ph.v4, lut, E, O, Eh, Oh);
+                                                   rs, re, kb + (uint32_t)(gl + c * G) < nch[u],
+                                                   ph.v4, E, O, Eh, Oh);
             }
 
             uint32_t S = combine(E, O, s[u] & 1);
