@@ -148,9 +148,15 @@ def make_workload(args, dev, rank, world):
     desc = f"C4: {n} packets, Zipf(s=1) lengths 64-1472 B (mean {nbytes / n:.1f}), packed"
     meta = {"packets_per_gpu": n, "mean_packet_bytes": round(nbytes / n, 2),
             "layout": "ragged", "kind": kind}
-    plan = {"kernel": "flat (chunk-balanced, 64-packet tiles)",
-            "rows_per_group": int(os.environ.get("WC_FLAT_UN", "2")),
-            "grid": int((n + 255) // 256)}
+    seg = int(os.environ.get("WC_SEG", "1"))
+    if seg >= 2 or (seg == 1 and kind == "ip"):
+        plan = {"kernel": "seg (segmented prefix over dense 64-packet tiles, flat fallback)",
+                "rows_per_group": int(os.environ.get("WC_SEG_ROWS", "4")),
+                "grid": int((n + 255) // 256)}
+    else:
+        plan = {"kernel": "flat (chunk-balanced, 64-packet tiles)",
+                "rows_per_group": int(os.environ.get("WC_FLAT_UN", "2")),
+                "grid": int((n + 255) // 256)}
     return step, n, nbytes, buf, out, plan, desc, meta, (offs, lens), "weak"
 
 

@@ -102,6 +102,78 @@ def test_ragged_random_placement(gpu):
     np.testing.assert_array_equal(got, c_oracle.cksum_ragged(buf, offs, lens, kind=0))
 
 
+def _sorted_layout(rng, n, lens, gap_max=0, overlap_max=0, lead=0):
+    """Packets in offset order: each starts `gap` bytes after the previous
+    end (gap in [-overlap_max, gap_max]; starts and ends stay non-decreasing)."""
+    offs = np.zeros(n, dtype=np.uint64)
+    pos, prev_end = lead, lead
+    for i in range(n):
+        g = int(rng.integers(-overlap_max, gap_max + 1)) if (gap_max or overlap_max) else 0
+        start = max(prev_end + g, int(offs[i - 1]) if i else lead)
+        offs[i] = start
+        prev_end = max(prev_end, start + int(lens[i]))
+    return offs, prev_end + 64
+
+
+DENSE_LAYOUTS = ["packed", "packed_tiny", "gaps", "gaps_wide", "overlap", "exact_groups",
+                 "jumbo", "with_empty"]
+
+
+@pytest.mark.parametrize("seg", ["0", "1", "2"])
+@pytest.mark.parametrize("layout", DENSE_LAYOUTS)
+def test_ragged_dense_tiles(gpu, monkeypatch, layout, seg):
+    """Ordered ragged layouts (the segmented-prefix path for dense tiles, the
+    flat path for the rest): packed at every alignment, small gaps, gaps wide
+    enough to make some tiles sparse, overlapping ordered packets, tiles
+    ending exactly on a row-group boundary, 65535-B packets and empty
+    packets -- every packet against the oracle.  WC_SEG: 0 = flat kernel,
+    1 = seg kernel for ip_cksum (the default), 2 = seg kernel for both kinds."""
+    monkeypatch.setenv("WC_SEG", seg)
+    rng = np.random.default_rng(sum(layout.encode()))
+    n = 6000
+    lens = rng.integers(1, 2001, n).astype(np.uint16)
+    kw = {}
+    if layout == "packed_tiny":
+        lens = rng.integers(1, 40, n).astype(np.uint16)
+    elif layout == "gaps":
+        kw = {"gap_max": 60}
+    elif layout == "gaps_wide":
+        kw = {"gap_max": 700}
+    elif layout == "overlap":
+        kw = {"overlap_max": 300, "gap_max": 20}
+    elif layout == "exact_groups":
+        lens[:] = 1024
+        n = 64 * 24
+        lens = lens[:n]
+    elif layout == "jumbo":
+        n = 200
+        lens = rng.integers(60000, 65536, n).astype(np.uint16)
+        lens[::7] = 65535
+    elif layout == "with_empty":
+        lens[rng.integers(0, n, 40)] = 0
+    offs, size = _sorted_layout(rng, n, lens, lead=int(rng.integers(0, 16)), **kw)
+    buf = rng.integers(0, 256, size, dtype=np.uint8)
+    for k in (0, 1):
+        if k == 1:
+            if layout in ("with_empty", "packed_tiny"):
+                continue  # payload_cksum needs len >= header length
+            # make every packet a plausible IP header (v4 IHL 5..15 or v6)
+            for o, ln in zip(offs.tolist(), lens.tolist()):
+                v6 = ln >= 40 and rng.random() < 0.5
+                ihl = int(rng.integers(5, min(15, ln // 4) + 1)) if ln >= 20 else 5
+                buf[o] = 0x60 if v6 else 0x40 | ihl
+            ok = np.array([(buf[o] >> 4 == 6 and ln >= 40) or (buf[o] >> 4 == 4 and ln >= 4 * (buf[o] & 15))
+                           for o, ln in zip(offs.tolist(), lens.tolist())])
+            sel = np.flatnonzero(ok)
+            o_k, l_k = offs[sel], lens[sel]
+        else:
+            o_k, l_k = offs, lens
+        got = host(wc.cksum_ragged(dev_u8(buf, gpu), to_dev(o_k, gpu), to_dev(l_k, gpu),
+                                   kind=k))
+        np.testing.assert_array_equal(got, c_oracle.cksum_ragged(buf, o_k, l_k, kind=k),
+                                      err_msg=f"{layout} kind {k}")
+
+
 @pytest.mark.parametrize("shape", ["64,2,1", "64,4,1", "32,2,1", "16,2,2"])
 def test_ragged_group_kernel(gpu, monkeypatch, shape):
     """The small-batch ragged group kernel (forced for every batch size):
@@ -236,7 +308,10 @@ def test_c3_mtu_sweep_full(gpu, L):
     np.testing.assert_array_equal(got, c_oracle.cksum_strided(hb, L, L, n, kind=0))
 
 
-def test_c4_zipf_full(gpu):
+@pytest.mark.parametrize("seg", ["1", "0"])
+def test_c4_zipf_full(gpu, monkeypatch, seg):
+    """C4 in full through the seg kernel (default) and the flat kernel."""
+    monkeypatch.setenv("WC_SEG", seg)
     lens = synth.zipf_lengths(1 << 24)
     offs = synth.packed_offsets(lens)
     total = int(offs[-1]) + int(lens[-1])

@@ -19,6 +19,8 @@ for c in ${CASES:-c2:ip c2:payload}; do
         c2) a="--config c2" ;;
         c4) a="--config c4" ;;
         slot) a="--config c3 --len 1500 --stride 2048 --offset 14" ;;
+        rslot) a="--config c3 --len 1500 --stride 2048 --offset 14 --ragged" ;;
+        rc2) a="--config c2 --ragged" ;;
         c3-*) a="--config c3 --len ${cfg#c3-}" ;;
     esac
     echo "== $c"

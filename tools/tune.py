@@ -100,9 +100,13 @@ def main():
             run = lambda: wc.cksum_ragged(buf, d_off, d_len, out=out, kind=args.kind)  # noqa: E731
 
     variants = [("" if v.strip() == "default" else v.strip()) for v in args.variants.split(";") if v.strip()] or [""]
-    base_env = {k: os.environ.get(k) for k in ("WC_SHAPE", "WC_NT", "WC_BLOCKS_PER_CU", "WC_GRID",
-                                                "WC_FLAT_UN", "WC_FLAT_TPW", "WC_DIAG_NOLOAD",
-                                                "WC_FLAT_MIN", "WC_RAGGED_SHAPE")}
+    # Every WC_* knob a variant may set is reset before the next variant runs.
+    knobs = {"WC_SHAPE", "WC_NT", "WC_BLOCKS_PER_CU", "WC_GRID", "WC_FLAT_UN", "WC_FLAT_TPW",
+             "WC_DIAG_NOLOAD", "WC_FLAT_MIN", "WC_RAGGED_SHAPE", "WC_VARIANT", "WC_SEG",
+             "WC_SEG_ROWS"}
+    knobs |= {kv.split("=", 1)[0] for v in variants for kv in v.split()}
+    knobs |= {k for k in os.environ if k.startswith("WC_") and k != "WC_NO_BUILD"}
+    base_env = {k: os.environ.get(k) for k in knobs}
 
     def apply(spec):
         for k, v in base_env.items():

@@ -222,6 +222,7 @@ struct Plan {
     wc::Shape shape;
     bool full;
     int grid;
+    int seg_rows = 0; // ragged: k_cksum_seg row-group size, 0 = flat kernel
 };
 
 Plan plan_strided(const Device &D, uint64_t base, uint64_t stride, uint32_t len,
@@ -240,15 +241,21 @@ Plan plan_strided(const Device &D, uint64_t base, uint64_t stride, uint32_t len,
     return p;
 }
 
-// Ragged batches take the chunk-balanced flat kernel (group = 0 marks it;
-// unroll = 64-chunk rows per ping-pong group, WC_FLAT_UN).  A host
-// zero-copy batch of at most kZcGroupMax packets takes the ragged group
-// kernel instead: a flat wave walks its 64-packet tile's rows one PCIe
-// latency at a time, the group kernel issues every packet's loads at once.
-// (Device-resident batches measured no better on the group kernel at any
-// size -- launch cost dominates small ones -- so WC_FLAT_MIN defaults to 0.)
-// The fused header pass (out_hdr) exists in the flat kernel only.
-Plan plan_ragged(const Device &D, uint64_t n, bool zero_copy = false, bool hdr = false)
+// Ragged batches take the segmented-prefix kernel k_cksum_seg (ip_cksum):
+// dense tiles stream their byte range, sparse ones take its flat path
+// (DESIGN.md section 4.3).  payload_cksum and the fused header pass
+// (out_hdr) take the chunk-balanced flat kernel (group = 0 marks both;
+// unroll = 64-chunk rows per ping-pong group, WC_FLAT_UN): the seg path's
+// per-packet header loads cost more than its stream saves there.  WC_SEG =
+// 0 forces the flat kernel, 2 takes the seg kernel for payload_cksum too;
+// WC_SEG_ROWS = 2 / 4 / 8 rows per seg row group.  A host zero-copy batch of
+// at most kZcGroupMax packets takes the ragged group kernel instead: a flat
+// wave walks its 64-packet tile's rows one PCIe latency at a time, the group
+// kernel issues every packet's loads at once.  (Device-resident batches
+// measured no better on the group kernel at any size -- launch cost
+// dominates small ones -- so WC_FLAT_MIN defaults to 0.)
+Plan plan_ragged(const Device &D, uint64_t n, int kind, bool zero_copy = false,
+                 bool hdr = false)
 {
     (void)D;
     Plan p;
@@ -264,15 +271,21 @@ Plan plan_ragged(const Device &D, uint64_t n, bool zero_copy = false, bool hdr =
     }
     p.shape = {0, 1, env_int("WC_FLAT_UN", 2)};
     p.grid = 0;
+    const int seg = env_int("WC_SEG", 1);
+    if (!hdr && !zero_copy && env_int("WC_DIAG_NOLOAD", 0) == 0 &&
+        (seg >= 2 || (seg == 1 && kind == WC_CKSUM_IP)))
+        p.seg_rows = env_int("WC_SEG_ROWS", 4);
     return p;
 }
 
 bool nontemporal() { return env_int("WC_NT", 1) != 0; }
 int flat_tpw() { return env_int("WC_FLAT_TPW", 1); }
 
-int run(const Device &D, const wc::LaunchArgs &a, const Plan &p, hipStream_t st)
+int run(const Device &D, const wc::LaunchArgs &args, const Plan &p, hipStream_t st)
 {
     (void)D;
+    wc::LaunchArgs a = args;
+    a.seg_rows = p.seg_rows;
     hipError_t e = p.shape.group == 0 ? wc::launch_flat(a, p.shape.unroll, st)
                                       : wc::launch_cksum(a, p.shape, p.grid, st);
     return hip_err(e);
@@ -314,7 +327,7 @@ int batch_ragged(const void *d_base, const uint64_t *d_off, const uint16_t *d_le
     int rc = ensure_device(&D);
     if (rc)
         return rc;
-    const Plan p = plan_ragged(*D, n, false, d_out_hdr != nullptr);
+    const Plan p = plan_ragged(*D, n, kind, false, d_out_hdr != nullptr);
     wc::LaunchArgs a{d_base, 0,     0,    d_off, d_len, n,
                      d_out,  d_bad, kind, true,  false, nontemporal(), flat_tpw(),
                      d_out_hdr, env_int("WC_DIAG_NOLOAD", 0) != 0};
@@ -430,7 +443,7 @@ int host_zero_copy(Device &D, const uint8_t *dbase, const uint64_t *h_off,
     ZeroCopy &Z = D.zc;
     memcpy(Z.h_off, h_off, n * 8);
     memcpy(Z.h_len, h_len, n * 2);
-    const Plan p = plan_ragged(D, n, true);
+    const Plan p = plan_ragged(D, n, kind, true);
     wc::LaunchArgs a{dbase, 0,       0,    Z.d_off, Z.d_len, n,
                      Z.d_out, nullptr, kind, true,    false,   nontemporal(),
                      flat_tpw()};
@@ -517,7 +530,7 @@ int host_pipeline(Device &D, const uint8_t *hb, bool registered, bool ascending,
                                hipMemcpyHostToDevice, st);
         if (e != hipSuccess)
             return hip_err(e);
-        const Plan p = plan_ragged(D, cnt);
+        const Plan p = plan_ragged(D, cnt, kind);
         wc::LaunchArgs a{P.d_bytes[slot], 0,    0,    P.d_off[slot], P.d_len[slot],
                          cnt,             P.d_out[slot], nullptr, kind, true,
                          false,           nontemporal(), flat_tpw()};

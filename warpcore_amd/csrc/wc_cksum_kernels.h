@@ -58,6 +58,7 @@ struct LaunchArgs {
     uint16_t *out_hdr;  // payload kind: also the IPv4 header checksums (or null)
     bool diag_noload;   // WC_DIAG_NOLOAD=1: timing-only flat build (wrong results)
     int variant = 0;    // WC_VARIANT: experimental kernel variants (A/B tuning)
+    int seg_rows = 0;   // ragged: 0 = flat kernel, else k_cksum_seg with 2/4/8-row groups
 };
 
 struct Shape {
@@ -70,8 +71,9 @@ struct Shape {
 // variant over WC_RAGGED_SHAPE_LIST.
 hipError_t launch_cksum(const LaunchArgs &a, const Shape &sh, int grid,
                         hipStream_t st);
-// Chunk-balanced kernel for ragged batches (rows = 64-chunk rows per
-// ping-pong group: 1, 2 or 4).
+// Ragged batches: a.seg_rows != 0 -> the segmented-prefix kernel (dense
+// tiles; the rest take its flat path), else the chunk-balanced flat kernel
+// (rows = 64-chunk rows per ping-pong group: 1, 2 or 4).
 hipError_t launch_flat(const LaunchArgs &a, int rows, hipStream_t st);
 hipError_t launch_synth(void *buf, uint64_t nbytes, uint64_t seed, int grid,
                         hipStream_t st);

@@ -578,9 +578,9 @@ __device__ __forceinline__ void flat_issue(FlatRows<UN> &R, FlatLds<UN> &L,
     }
 }
 
-template <int UN, int KIND>
+template <int UN, int KIND, bool ARITH = false>
 __device__ __forceinline__ void flat_accum(const FlatRows<UN> &R, FlatLds<UN> &L,
-                                           const WeightLut &M, uint32_t g0,
+                                           const WeightLut *M, uint32_t g0,
                                            int lane, uint32_t cp, uint32_t ce,
                                            uint32_t total, uint32_t &acc)
 {
@@ -591,8 +591,12 @@ __device__ __forceinline__ void flat_accum(const FlatRows<UN> &R, FlatLds<UN> &L
         const FlatDesc &g = L.desc[R.own[u]];
         const uint32_t rel = g.rel, info = g.info;
         uint32_t E = 0, O = 0;
-        accum_masked<KIND>(R.d[u], (int)(16u * q - rel), (int)((info >> 16) & 0xFFu),
-                           (int)(info & 0xFFFFu), (info >> 24) & 1u, M, E, O);
+        if constexpr (ARITH)
+            accum_arith<KIND>(R.d[u], (int)(16u * q - rel), (int)((info >> 16) & 0xFFu),
+                              (int)(info & 0xFFFFu), (info >> 24) & 1u, E, O);
+        else
+            accum_masked<KIND>(R.d[u], (int)(16u * q - rel), (int)((info >> 16) & 0xFFu),
+                               (int)(info & 0xFFFFu), (info >> 24) & 1u, *M, E, O);
         P[u] = q < total ? combine(E, O, rel & 1u) : 0u;
     }
     // Inclusive prefix sums of the UN rows, step-interleaved so each row's DPP
@@ -653,6 +657,66 @@ __device__ __forceinline__ uint16_t lane_hdr_cksum(uint64_t a, uint32_t hl,
     return fold_not(combine(E, O, s & 1u));
 }
 
+// One 64-packet tile of the flat kernel: returns this lane's packet's exact
+// reference accumulator (in_cksum.c:140-167 / 107-120, mod 2^32) -- the
+// caller folds it.  `after_first_issue` runs once the tile's first row group
+// is in flight (the caller's next-tile prefetch goes there).
+template <int UN, int KIND, bool NT, bool NOLOAD, bool ARITH, class F>
+__device__ __forceinline__ uint32_t flat_tile_sum(FlatLds<UN> &L, const WeightLut *lut,
+                                                  int lane, uint64_t a, uint32_t len,
+                                                  bool valid, const PseudoHdr &ph,
+                                                  F &&after_first_issue)
+{
+    const uint32_t s = (uint32_t)(a & 15u);
+    const uint32_t span = KIND == WC_KIND_PAYLOAD ? max(len, 20u) : len;
+    const uint32_t nch = valid ? (s + span + 15u) >> 4 : 0u;
+
+    // Chunk-slot range [cp, ce) of this lane's packet within the tile;
+    // rank among the tile's non-empty packets.
+    const uint32_t ce = wave_incl_sum(nch);
+    const uint32_t cp = ce - nch;
+    const uint32_t total = __shfl(ce, 63, 64);
+    const uint64_t nonempty = __ballot(nch != 0);
+    const uint32_t rank = mbcnt64(nonempty);
+    const uint32_t last_rank = nonempty ? (uint32_t)__builtin_popcountll(nonempty) - 1u : 0u;
+    const uint64_t vb = (a & ~15ull) - 16ull * cp;
+    if (nch != 0)
+        L.desc[rank] = FlatDesc{(uint32_t)vb, (uint32_t)(vb >> 32), s + 16u * cp,
+                                len | (ph.hl << 16) | (ph.v4 << 24)};
+    // Row marks carry the row's number within the tile; reset them to a
+    // tag no row has so the previous tile's marks can't match.
+#pragma unroll
+    for (int u = 0; u < UN; ++u)
+        L.mark[u][lane] = 0xFFFFFFFFu;
+    wave_order();
+
+    uint32_t acc = ph.special;
+    constexpr uint32_t kGrp = 64u * UN;
+    FlatRows<UN> A, B;
+    if (total != 0)
+        flat_issue<UN, NT, NOLOAD>(A, L, 0, lane, cp, ce, rank, last_rank, total);
+    after_first_issue();
+    if (total != 0) {
+        // Ping-pong row groups A / B (no register copies): group g+1's
+        // loads are in flight while group g is summed.  No exit between
+        // the halves: a half past the tile's end sums zeros, and keeping
+        // each load's use in the next half stops hipcc sinking the load
+        // next to it; sched_barrier keeps each issue ahead of the other
+        // group's sum.
+        for (uint32_t j = 0; j < total; j += 2 * kGrp) {
+            flat_issue<UN, NT, NOLOAD>(B, L, j + kGrp, lane, cp, ce, rank, last_rank, total);
+            __builtin_amdgcn_sched_barrier(0);
+            flat_accum<UN, KIND, ARITH>(A, L, lut, j, lane, cp, ce, total, acc);
+            __builtin_amdgcn_sched_barrier(0);
+            flat_issue<UN, NT, NOLOAD>(A, L, j + 2 * kGrp, lane, cp, ce, rank, last_rank, total);
+            __builtin_amdgcn_sched_barrier(0);
+            flat_accum<UN, KIND, ARITH>(B, L, lut, j + kGrp, lane, cp, ce, total, acc);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    return acc;
+}
+
 template <int UN, int KIND, bool NT, bool HDR, bool NOLOAD = false>
 __global__ void __launch_bounds__(256)
 k_cksum_flat(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
@@ -694,61 +758,18 @@ k_cksum_flat(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
         len_n = valid_n ? (uint32_t)lens[pn] : 0u;
 
         const uint64_t a = (uint64_t)base + off;
-        const uint32_t s = (uint32_t)(a & 15u);
-        const uint32_t span = KIND == WC_KIND_PAYLOAD ? max(len, 20u) : len;
-        const uint32_t nch = valid ? (s + span + 15u) >> 4 : 0u;
         PseudoHdr ph{0u, 1u, 0u};
         if constexpr (KIND == WC_KIND_PAYLOAD)
             if (valid)
                 ph = pseudo_hdr(hdr4 & 0xFFu, (hdr4 >> 8) & 0xFFu, (hdr4 >> 16) & 0xFFu,
                                 hdr4 >> 24);
-
-        // Chunk-slot range [cp, ce) of this lane's packet within the tile;
-        // rank among the tile's non-empty packets.
-        const uint32_t ce = wave_incl_sum(nch);
-        const uint32_t cp = ce - nch;
-        const uint32_t total = __shfl(ce, 63, 64);
-        const uint64_t nonempty = __ballot(nch != 0);
-        const uint32_t rank = mbcnt64(nonempty);
-        const uint32_t last_rank = nonempty ? (uint32_t)__builtin_popcountll(nonempty) - 1u : 0u;
-        const uint64_t vb = (a & ~15ull) - 16ull * cp;
-        if (nch != 0)
-            L.desc[rank] = FlatDesc{(uint32_t)vb, (uint32_t)(vb >> 32), s + 16u * cp,
-                                    len | (ph.hl << 16) | (ph.v4 << 24)};
-        // Row marks carry the row's number within the tile; reset them to a
-        // tag no row has so the previous tile's marks can't match.
-#pragma unroll
-        for (int u = 0; u < UN; ++u)
-            L.mark[u][lane] = 0xFFFFFFFFu;
-        wave_order();
-
-        uint32_t acc = ph.special;
-        constexpr uint32_t kGrp = 64u * UN;
-        FlatRows<UN> A, B;
-        if (total != 0)
-            flat_issue<UN, NT, NOLOAD>(A, L, 0, lane, cp, ce, rank, last_rank, total);
         // The next tile's header bytes: issued once its offsets are back,
         // behind this tile's first loads.
-        if constexpr (KIND == WC_KIND_PAYLOAD)
-            hdr_n = valid_n ? load_hdr4((uint64_t)base + off_n) : 0u;
-        if (total != 0) {
-            // Ping-pong row groups A / B (no register copies): group g+1's
-            // loads are in flight while group g is summed.  No exit between
-            // the halves: a half past the tile's end sums zeros, and keeping
-            // each load's use in the next half stops hipcc sinking the load
-            // next to it; sched_barrier keeps each issue ahead of the other
-            // group's sum.
-            for (uint32_t j = 0; j < total; j += 2 * kGrp) {
-                flat_issue<UN, NT, NOLOAD>(B, L, j + kGrp, lane, cp, ce, rank, last_rank, total);
-                __builtin_amdgcn_sched_barrier(0);
-                flat_accum<UN, KIND>(A, L, lut, j, lane, cp, ce, total, acc);
-                __builtin_amdgcn_sched_barrier(0);
-                flat_issue<UN, NT, NOLOAD>(A, L, j + 2 * kGrp, lane, cp, ce, rank, last_rank, total);
-                __builtin_amdgcn_sched_barrier(0);
-                flat_accum<UN, KIND>(B, L, lut, j + kGrp, lane, cp, ce, total, acc);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        }
+        const uint32_t acc = flat_tile_sum<UN, KIND, NT, NOLOAD, false>(
+            L, &lut, lane, a, len, valid, ph, [&] {
+                if constexpr (KIND == WC_KIND_PAYLOAD)
+                    hdr_n = valid_n ? load_hdr4((uint64_t)base + off_n) : 0u;
+            });
 
         const uint16_t r = fold_not(acc);
         if (valid && out)
@@ -757,6 +778,337 @@ k_cksum_flat(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
         if constexpr (HDR)
             if (valid)
                 out_hdr[p] = ph.v4 ? lane_hdr_cksum<NT>(a, ph.hl, lut) : 0;
+        wave_order(); // the tables are rewritten by the next tile
+    }
+    if (bad) {
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1)
+            nbad += __shfl_xor(nbad, m, 64);
+        if (lane == 0 && nbad)
+            atomicAdd(bad, (unsigned long long)nbad);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Ragged batches, dense tiles: the "segmented prefix" path.
+//
+// When a tile's 64 packets lie in order inside one dense byte range (starts
+// and ends non-decreasing, gaps < 4 KiB, range <= 9/8 of the tile's bytes +
+// 2 KiB -- the packed Zipf layout of C4, an RX ring drained into one buffer),
+// the wave streams that range itself: row r of the tile is the 64 chunks
+// [A0 + 1024 r, + 1024), every load fully coalesced and its address known
+// without any per-chunk owner lookup.  Every chunk is summed with constant
+// weights, a wave prefix sum gives the running sum at every chunk boundary,
+// and each packet lane takes the difference of the running sums at its end
+// and its start, adding its partial first / last chunk from its own cached
+// re-load.  Bytes outside every packet cancel in the differences.  A gap of
+// less than 4 KiB between two packets lies in pages that hold packet bytes,
+// so the stream never touches an unmapped page.  Other tiles take the flat
+// path above.
+//
+// ip_cksum needs ONE running sum: V = sum of the little-endian words at even
+// addresses (v_dot2_u32_u16, 4 per chunk).  For an even-start packet V is the
+// reference's accumulator (in_cksum.c:107-120; < 2^31, no wrap).  For an odd
+// start the reference's X = O + 256 E satisfies X == 256 V == rotl32(V, 8)
+// (mod 0xFFFF, as 2^16 == 2^32 == 1) and X == 0 iff V == 0; the end-around
+// fold (in_cksum.c:74-80) maps positive numbers to [1, 0xFFFF] by their
+// residue, so fold(rotl32(V, 8)) is bit-exact.  payload_cksum adds terms that
+// can wrap the uint32 (next_hdr << 24, in_cksum.c:157), so it keeps the exact
+// byte-lane sums E and O instead (two running sums).
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t wsum(uint32_t x, uint32_t acc)
+{
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, x), u16x2{1, 1}, acc, false);
+}
+
+// 0xFF in the bytes of dword j that are among the first q bytes of a chunk.
+__device__ __forceinline__ uint32_t head_mask(uint32_t q, int j)
+{
+    const uint32_t nb = min(q - min(q, 4u * j), 4u);
+    return nb >= 4u ? 0xFFFFFFFFu : ((1u << (8u * nb)) - 1u);
+}
+
+template <int KIND>
+struct SegSum {
+    static constexpr int NV = KIND == WC_KIND_PAYLOAD ? 2 : 1;
+    uint32_t v[NV];
+};
+
+// Sum of a chunk's first q bytes (q = 16: all of them).
+template <int KIND, bool MASK>
+__device__ __forceinline__ SegSum<KIND> seg_chunk(const u32x4 &d, uint32_t q)
+{
+    SegSum<KIND> r;
+#pragma unroll
+    for (int i = 0; i < SegSum<KIND>::NV; ++i)
+        r.v[i] = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t x = MASK ? pick_dword(d, j) & head_mask(q, j) : pick_dword(d, j);
+        if constexpr (KIND == WC_KIND_PAYLOAD) {
+            r.v[0] = dot4(x, kEvenW, r.v[0]);
+            r.v[1] = dot4(x, kOddW, r.v[1]);
+        } else {
+            r.v[0] = wsum(x, r.v[0]);
+        }
+    }
+    return r;
+}
+
+template <int UNS>
+struct SegRows {
+    u32x4 d[UNS];
+};
+
+template <int UNS, bool NT>
+__device__ __forceinline__ void seg_issue(SegRows<UNS> &R, uint64_t A0, uint32_t g0, int lane,
+                                          uint32_t T, uint64_t zero)
+{
+#pragma unroll
+    for (int u = 0; u < UNS; ++u) {
+        const uint32_t q = g0 + 64u * u + (uint32_t)lane;
+        R.d[u] = load_chunk<NT>(q < T ? A0 + 16ull * q : zero);
+    }
+}
+
+// Sum the UNS rows of the group at slot g0: row prefix sums (DPP), chained
+// through LDS; packet lanes whose start / end chunk falls in the group pick
+// up the running sum before it.  `carry` is the running sum before the group
+// (wave-uniform).
+template <int UNS, int KIND>
+__device__ __forceinline__ void seg_accum(const SegRows<UNS> &R, uint32_t *pre, u32x4 *stage,
+                                          uint32_t g0, int lane, uint32_t cs, uint32_t ce,
+                                          SegSum<KIND> &carry, SegSum<KIND> &Ps,
+                                          SegSum<KIND> &Pe, u32x4 &hs, u32x4 &he)
+{
+    constexpr int NV = SegSum<KIND>::NV;
+    constexpr uint32_t kGrp = 64u * UNS;
+    uint32_t P[UNS][NV];
+#pragma unroll
+    for (int u = 0; u < UNS; ++u) {
+        const SegSum<KIND> c = seg_chunk<KIND, false>(R.d[u], 16u);
+#pragma unroll
+        for (int i = 0; i < NV; ++i)
+            P[u][i] = c.v[i];
+    }
+#define WC_SEG_STEP(CTRL, ROWS)                                                \
+    _Pragma("unroll") for (int u = 0; u < UNS; ++u)                            \
+        _Pragma("unroll") for (int i = 0; i < NV; ++i)                         \
+            P[u][i] += dpp0<CTRL, ROWS>(P[u][i]);
+    WC_SEG_STEP(kDppRowShr + 1, 0xF)
+    WC_SEG_STEP(kDppRowShr + 2, 0xF)
+    WC_SEG_STEP(kDppRowShr + 4, 0xF)
+    WC_SEG_STEP(kDppRowShr + 8, 0xF)
+    WC_SEG_STEP(kDppRowBcast15, 0xA)
+    WC_SEG_STEP(kDppRowBcast31, 0xC)
+#undef WC_SEG_STEP
+    uint32_t c[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+        c[i] = carry.v[i];
+#pragma unroll
+    for (int u = 0; u < UNS; ++u) {
+        stage[64u * u + lane] = R.d[u];
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+            const uint32_t tot = __builtin_amdgcn_readlane(P[u][i], 63);
+            pre[i * kGrp + 64u * u + lane] = P[u][i] + c[i];
+            c[i] += tot;
+        }
+    }
+    wave_order();
+    const uint32_t ds = cs - g0, de = ce - g0;
+    // The packet's first / last chunk, for its partial sums (exec-masked
+    // LDS reads: no scattered global re-loads).
+    if (ds < kGrp)
+        hs = stage[ds];
+    if (de < kGrp)
+        he = stage[de];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        const uint32_t vs = pre[i * kGrp + min(ds - 1u, kGrp - 1u)];
+        const uint32_t ve = pre[i * kGrp + min(de - 1u, kGrp - 1u)];
+        if (ds < kGrp)
+            Ps.v[i] = ds ? vs : carry.v[i];
+        if (de < kGrp)
+            Pe.v[i] = de ? ve : carry.v[i];
+        carry.v[i] = c[i];
+    }
+    wave_order(); // pre is rewritten by the next group
+}
+
+// One dense tile.  [a, a + len) is this lane's packet (payload: the whole IP
+// packet, header included -- the header is taken out again below, so the
+// stream never waits for the header bytes).  Returns the checksum.
+template <int UNS, int KIND, bool NT, class F>
+__device__ __forceinline__ uint16_t seg_tile(uint32_t *pre, u32x4 *stage, int lane, uint64_t a,
+                                             uint32_t len,
+                                             const PseudoHdr &ph, uint64_t A0, uint32_t T,
+                                             uint64_t zero, F &&after_first_issue)
+{
+    constexpr int NV = SegSum<KIND>::NV;
+    constexpr uint32_t kGrp = 64u * UNS;
+    const uint64_t rs = a - A0, re = rs + len;
+    const uint32_t cs = (uint32_t)(rs >> 4), qs = (uint32_t)(rs & 15u);
+    const uint32_t ce = (uint32_t)(re >> 4), qe = (uint32_t)(re & 15u);
+
+    SegRows<UNS> A, B;
+    seg_issue<UNS, NT>(A, A0, 0, lane, T, zero);
+    after_first_issue();
+    // For payload_cksum: the packet's header chunks.
+    u32x4 hs = {0u, 0u, 0u, 0u}, he = {0u, 0u, 0u, 0u};
+    constexpr int NH = KIND == WC_KIND_PAYLOAD ? 5 : 0; // [0, 60) from any phase
+    u32x4 hc[NH > 0 ? NH : 1];
+    const uint32_t s = (uint32_t)(a & 15u);
+    if constexpr (NH > 0) {
+        const uint32_t nspan = (s + max(len, 20u) + 15u) >> 4;
+#pragma unroll
+        for (int k = 0; k < NH; ++k)
+            hc[k] = load_chunk<false>((uint32_t)k < nspan ? (a & ~15ull) + 16ull * k : zero);
+    }
+
+    SegSum<KIND> carry, Ps, Pe;
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+        carry.v[i] = Ps.v[i] = Pe.v[i] = 0;
+    uint32_t j = 0;
+    for (; j < T; j += 2 * kGrp) {
+        seg_issue<UNS, NT>(B, A0, j + kGrp, lane, T, zero);
+        __builtin_amdgcn_sched_barrier(0);
+        seg_accum<UNS, KIND>(A, pre, stage, j, lane, cs, ce, carry, Ps, Pe, hs, he);
+        __builtin_amdgcn_sched_barrier(0);
+        seg_issue<UNS, NT>(A, A0, j + 2 * kGrp, lane, T, zero);
+        __builtin_amdgcn_sched_barrier(0);
+        seg_accum<UNS, KIND>(B, pre, stage, j + kGrp, lane, cs, ce, carry, Ps, Pe, hs, he);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    if (ce >= j) // the packet ends exactly at the last row group's end
+#pragma unroll
+        for (int i = 0; i < NV; ++i)
+            Pe.v[i] = carry.v[i];
+
+    const SegSum<KIND> ps = seg_chunk<KIND, true>(hs, qs);
+    const SegSum<KIND> pe = seg_chunk<KIND, true>(he, qe);
+    uint32_t v[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+        v[i] = (Pe.v[i] + pe.v[i]) - (Ps.v[i] + ps.v[i]);
+    if constexpr (KIND == WC_KIND_PAYLOAD) {
+        // payload = packet - header [0, hl) + pseudo-header fields (whose
+        // bytes inside the header thus count once, outside it twice -- the
+        // reference's own result for a malformed IHL < 5).  len < hl (no
+        // payload; the reference would read 4 GiB): fields only, as the flat
+        // path computes it.
+        uint32_t Ef = 0, Of = 0, Eh = 0, Oh = 0;
+#pragma unroll
+        for (int k = 0; k < NH; ++k) {
+            const int co = 16 * k - (int)s;
+            accum_arith<WC_KIND_PAYLOAD>(hc[k], co, 0, 0, ph.v4, Ef, Of);
+            accum_arith<WC_KIND_IP>(hc[k], co, 0, (int)ph.hl, 0u, Eh, Oh);
+        }
+        const bool body = len >= ph.hl;
+        const uint32_t E = (body ? v[0] - Eh : 0u) + Ef;
+        const uint32_t O = (body ? v[1] - Oh : 0u) + Of;
+        return fold_not(combine(E, O, a & 1u) + ph.special);
+    } else {
+        return fold_not((a & 1u) ? __builtin_amdgcn_alignbit(v[0], v[0], 24) : v[0]);
+    }
+}
+
+// Dense-tile test (wave-uniform): every valid packet non-empty, starts and
+// ends non-decreasing, gaps below 4 KiB, and the range at most 9/8 of the
+// tile's bytes + 2 KiB.  Sets the range [A0, A0 + 16 T).
+__device__ __forceinline__ bool seg_dense(int lane, uint64_t a, uint32_t len, bool valid,
+                                          uint32_t nvalid, uint64_t &A0, uint32_t &T)
+{
+    const uint64_t e = a + len;
+    const uint64_t elast = __shfl(e, (int)nvalid - 1, 64);
+    const uint64_t s0 = valid ? a : elast, s1 = valid ? e : elast;
+    const uint64_t p0 = __shfl_up(s0, 1, 64), p1 = __shfl_up(s1, 1, 64);
+    const bool ok = !valid || (len != 0 && (lane == 0 ||
+                                            (s0 >= p0 && s1 >= p1 && s0 < p1 + 4096u)));
+    if (__ballot(!ok))
+        return false;
+    const uint32_t sum = __shfl(wave_incl_sum(valid ? len : 0u), 63, 64);
+    A0 = __shfl(s0, 0, 64) & ~15ull;
+    const uint64_t range = elast - A0;
+    if (range > (uint64_t)sum + sum / 8u + 2048u)
+        return false;
+    T = (uint32_t)((range + 15u) >> 4);
+    return true;
+}
+
+// Ragged kernel with both paths: dense tiles stream their byte range
+// (seg_tile), the others take the flat path.  (The fused header checksum
+// stays on k_cksum_flat.)
+template <int UN, int UNS, int KIND, bool NT>
+__global__ void __launch_bounds__(256)
+k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
+            const uint16_t *__restrict__ lens, uint64_t n, uint16_t *__restrict__ out,
+            unsigned long long *__restrict__ bad)
+{
+    constexpr int NV = SegSum<KIND>::NV;
+    union TileLds {
+        FlatLds<UN> flat;
+        struct {
+            u32x4 stage[64 * UNS]; // the row group's chunks
+            uint32_t pre[NV * 64 * UNS];
+        } seg;
+    };
+    __shared__ TileLds lds_all[kFlatWaves];
+
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    TileLds &L = lds_all[w];
+    const uint64_t ntiles = (n + 63) / 64;
+    const uint64_t nwaves = (uint64_t)gridDim.x * kFlatWaves;
+    uint64_t tile = (uint64_t)blockIdx.x * kFlatWaves + w;
+    uint32_t nbad = 0;
+    const uint64_t zero = (uint64_t)(uintptr_t)&kZeroChunk;
+
+    uint64_t p = tile * 64 + lane;
+    uint64_t off_n = p < n ? offs[p] : 0;
+    uint32_t len_n = p < n ? (uint32_t)lens[p] : 0u;
+    uint32_t hdr_n = 0;
+    if constexpr (KIND == WC_KIND_PAYLOAD)
+        hdr_n = p < n ? load_hdr4((uint64_t)base + off_n) : 0u;
+
+    for (; tile < ntiles; tile += nwaves) {
+        p = tile * 64 + lane;
+        const bool valid = p < n;
+        const uint32_t nvalid = (uint32_t)min<uint64_t>(64, n - tile * 64);
+        const uint64_t off = off_n;
+        const uint32_t len = len_n;
+        const uint32_t hdr4 = hdr_n;
+        const uint64_t pn = (tile + nwaves) * 64 + lane;
+        const bool valid_n = pn < n;
+        off_n = valid_n ? offs[pn] : 0;
+        len_n = valid_n ? (uint32_t)lens[pn] : 0u;
+        auto prefetch_hdr = [&] {
+            if constexpr (KIND == WC_KIND_PAYLOAD)
+                hdr_n = valid_n ? load_hdr4((uint64_t)base + off_n) : 0u;
+        };
+
+        const uint64_t a = (uint64_t)base + off;
+        PseudoHdr ph{0u, 1u, 0u};
+        if constexpr (KIND == WC_KIND_PAYLOAD)
+            if (valid)
+                ph = pseudo_hdr(hdr4 & 0xFFu, (hdr4 >> 8) & 0xFFu, (hdr4 >> 16) & 0xFFu,
+                                hdr4 >> 24);
+        uint64_t A0 = 0;
+        uint32_t T = 0;
+        uint16_t r;
+        if (seg_dense(lane, a, len, valid, nvalid, A0, T))
+            r = seg_tile<UNS, KIND, NT>(L.seg.pre, L.seg.stage, lane, a, len, ph, A0, T, zero,
+                                        prefetch_hdr);
+        else
+            r = fold_not(flat_tile_sum<UN, KIND, NT, false, true>(L.flat, nullptr, lane, a, len,
+                                                                  valid, ph, prefetch_hdr));
+        if (valid && out)
+            out[p] = r;
+        nbad += valid && r != 0;
         wave_order(); // the tables are rewritten by the next tile
     }
     if (bad) {
@@ -875,6 +1227,24 @@ static hipError_t launch_flat_un(const LaunchArgs &a, hipStream_t st)
     if (a.diag_noload && a.kind == WC_KIND_IP) {
         hipLaunchKernelGGL((k_cksum_flat<UN, WC_KIND_IP, true, false, true>), dim3(grid),
                            dim3(256), 0, st, b, a.offs, a.lens, a.n, a.out, bad, a.out_hdr);
+        return hipGetLastError();
+    }
+    if (a.seg_rows && !a.out_hdr) {
+#define WC_SEG(US)                                                             \
+    if (a.kind == WC_KIND_PAYLOAD)                                             \
+        hipLaunchKernelGGL((k_cksum_seg<UN, US, WC_KIND_PAYLOAD, true>), dim3(grid), \
+                           dim3(256), 0, st, b, a.offs, a.lens, a.n, a.out, bad); \
+    else                                                                       \
+        hipLaunchKernelGGL((k_cksum_seg<UN, US, WC_KIND_IP, true>), dim3(grid), \
+                           dim3(256), 0, st, b, a.offs, a.lens, a.n, a.out, bad);
+        if (a.seg_rows == 2) {
+            WC_SEG(2)
+        } else if (a.seg_rows == 8) {
+            WC_SEG(8)
+        } else {
+            WC_SEG(4)
+        }
+#undef WC_SEG
         return hipGetLastError();
     }
     if (a.kind == WC_KIND_PAYLOAD && a.out_hdr) {
