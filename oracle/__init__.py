@@ -11,5 +11,7 @@ leg.  It is the checker, never the thing measured or shipped.
 
 Reference restated: /root/reference/lib/src/in_cksum.c:74-167.
 Parity status: see wc_oracle.h and DESIGN.md section 3 ("parity unpinned"
-except for the known answers in tests/golden/kat.json).
+against the reference except for the known answers in tests/golden/kat.json;
+the standard arithmetic is also pinned by Linux-kernel-computed checksums in
+tests/golden/linux_vectors.npz).
 """

@@ -6,10 +6,12 @@
  * the HIP kernels and the timed CPU baseline; it is never linked into the
  * product library.
  *
- * Parity: "parity unpinned" except for the known answers in
- * tests/golden/kat.json (recorded by SURVEY.md/BASELINE.md from the compiled
- * reference object) -- the reference itself is unbuildable here because
- * in_cksum.c needs the CMake-generated <warpcore/config.h>.
+ * Parity: "parity unpinned" against the reference except for the known
+ * answers in tests/golden/kat.json (recorded by SURVEY.md/BASELINE.md from the
+ * compiled reference object) -- the reference itself is unbuildable here
+ * because in_cksum.c needs the CMake-generated <warpcore/config.h>.  The
+ * standard arithmetic is also pinned by Linux-kernel-computed checksums
+ * (tests/golden/linux_vectors.npz).
  */
 #define _GNU_SOURCE
 #include "wc_oracle.h"

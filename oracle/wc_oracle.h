@@ -19,7 +19,11 @@
  * <warpcore/config.h>, which only CMake generates), so this restatement is
  * pinned only by the known answers SURVEY.md / BASELINE.md recorded from the
  * compiled reference (tests/golden/kat.json) and by external RFC examples.
- * Everything else is "parity unpinned" -- see DESIGN.md section 3.
+ * Everything else is "parity unpinned" against the reference -- see DESIGN.md
+ * section 3.  The standard RFC 1071 arithmetic (word sum, fold, byte order,
+ * IPv4 / IPv6 pseudo-headers with next header 17) is additionally pinned by
+ * checksums the Linux kernel computed on the same bytes
+ * (tests/golden/linux_vectors.npz, make_kernel_vectors.py).
  */
 #pragma once
 

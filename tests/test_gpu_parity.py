@@ -75,6 +75,18 @@ SWEEP_LENS = list(range(0, 131)) + [255, 256, 257, 511, 575, 576, 577, 1471, 147
                                     1473, 2048, 4095, 8999, 9000, 9001, 65535]
 
 
+@pytest.mark.parametrize("group,kind", [("icmp", 0), ("ip4hdr", 0), ("udp6", 1), ("udp4", 1)])
+def test_linux_kernel_vectors(gpu, group, kind):
+    """Checksums computed (or accepted) by the Linux kernel's RFC 1071 code on
+    the same bytes: ICMP echo replies, IPv4 headers, UDP over IPv6 / IPv4
+    (tests/golden/make_kernel_vectors.py) -- an implementation independent of
+    this project and of the reference."""
+    g = np.load(GOLDEN / "linux_vectors.npz")
+    out = wc.cksum_ragged(dev_u8(g[group + "_blob"], gpu), to_dev(g[group + "_off"], gpu),
+                          to_dev(g[group + "_len"], gpu), kind=kind)
+    np.testing.assert_array_equal(host(out), g[group + "_expect"])
+
+
 @pytest.mark.parametrize("length", SWEEP_LENS)
 def test_strided_sweep(gpu, length):
     rng = np.random.default_rng(length)

@@ -47,6 +47,23 @@ def test_golden_vectors_payload():
     np.testing.assert_array_equal(got, g["pl_expect"])
 
 
+LINUX_GROUPS = [("icmp", 0), ("ip4hdr", 0), ("udp6", 1), ("udp4", 1)]
+
+
+@pytest.mark.parametrize("group,kind", LINUX_GROUPS)
+def test_linux_kernel_vectors(group, kind):
+    """Both restatements reproduce checksums the Linux kernel computed (or,
+    for udp4, accepted) on the same bytes -- tests/golden/make_kernel_vectors.py."""
+    g = np.load(GOLDEN / "linux_vectors.npz")
+    blob, offs, lens = g[group + "_blob"], g[group + "_off"], g[group + "_len"]
+    got = c_oracle.cksum_ragged(blob, offs, lens, kind=kind)
+    np.testing.assert_array_equal(got, g[group + "_expect"])
+    b = blob.tobytes()
+    fn = py_oracle.payload_cksum if kind else py_oracle.ip_cksum
+    for o, n, e in list(zip(offs.tolist(), lens.tolist(), g[group + "_expect"].tolist()))[:60]:
+        assert fn(b[o:o + n], n) == e
+
+
 def test_c_vs_py_ip_sweep():
     rng = np.random.default_rng(1)
     blob = rng.integers(0, 256, 20000, dtype=np.uint8)
