@@ -53,7 +53,9 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
         if _lib is not None:
             return _lib
         path = _build.LIB
-        if build_if_missing and os.environ.get("WC_NO_BUILD") != "1":
+        if os.environ.get("WC_LIB"):  # A/B tuning of two builds (tools/)
+            path = _build.Path(os.environ["WC_LIB"])
+        elif build_if_missing and os.environ.get("WC_NO_BUILD") != "1":
             _build.build_lib()
         if not path.exists():
             raise RuntimeError(

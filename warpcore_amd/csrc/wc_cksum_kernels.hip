@@ -65,7 +65,6 @@ __device__ __forceinline__ uint32_t pick_byte(const u32x4 &d, int pos)
 // Global (addrspace 1) pointer: lets hipcc emit global_load_dwordx4 rather
 // than flat loads for addresses computed as integers.
 typedef const u32x4 __attribute__((address_space(1))) *gchunk_ptr;
-typedef const uint8_t __attribute__((address_space(1))) *gbyte_ptr;
 
 template <bool NT>
 __device__ __forceinline__ u32x4 load_chunk(uint64_t addr)
@@ -631,12 +630,20 @@ __device__ __forceinline__ void flat_accum(const FlatRows<UN> &R, FlatLds<UN> &L
 }
 
 // Header bytes 0, 2, 3, 6 of a packet (payload_cksum), packed b0 | b2 << 8 |
-// b3 << 16 | b6 << 24.
+// b3 << 16 | b6 << 24.  ONE 16-byte load from the 8-byte boundary at or below
+// the packet start (a scattered load moves a whole cache line per lane, so
+// one load instead of four byte loads): [a & ~7, +16) lies in a's own 8-byte
+// block or within the 20 header bytes payload_cksum reads anyway
+// (in_cksum.c:149-151), so it never touches a page the reference would not.
+typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 __device__ __forceinline__ uint32_t load_hdr4(uint64_t a)
 {
-    gbyte_ptr h = (gbyte_ptr)(uintptr_t)a;
-    return (uint32_t)h[0] | ((uint32_t)h[2] << 8) | ((uint32_t)h[3] << 16) |
-           ((uint32_t)h[6] << 24);
+    const u32x4a4 d = *(const u32x4a4 __attribute__((address_space(1))) *)(uintptr_t)(a & ~7ull);
+    const uint32_t sh = 8u * (uint32_t)(a & 7u);
+    const uint64_t lo = (uint64_t)d.x | ((uint64_t)d.y << 32);
+    const uint64_t hi = (uint64_t)d.z | ((uint64_t)d.w << 32);
+    const uint64_t w = sh ? (lo >> sh) | (hi << (64u - sh)) : lo; // packet bytes 0..7
+    return __builtin_amdgcn_perm((uint32_t)(w >> 32), (uint32_t)w, 0x06030200u);
 }
 
 // Fused IPv4 header checksum for the flat kernel: the packet's own lane sums
