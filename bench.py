@@ -149,7 +149,7 @@ def make_workload(args, dev, rank, world):
     meta = {"packets_per_gpu": n, "mean_packet_bytes": round(nbytes / n, 2),
             "layout": "ragged", "kind": kind}
     seg = int(os.environ.get("WC_SEG", "1"))
-    if seg >= 2 or (seg == 1 and kind == "ip"):
+    if seg != 0:
         plan = {"kernel": "seg (segmented prefix over dense 64-packet tiles, flat fallback)",
                 "rows_per_group": int(os.environ.get("WC_SEG_ROWS", "4")),
                 "grid": int((n + 255) // 256)}

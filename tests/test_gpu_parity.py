@@ -131,7 +131,7 @@ DENSE_LAYOUTS = ["packed", "packed_tiny", "gaps", "gaps_wide", "overlap", "exact
                  "jumbo", "with_empty"]
 
 
-@pytest.mark.parametrize("seg", ["0", "1", "2"])
+@pytest.mark.parametrize("seg", ["0", "1"])
 @pytest.mark.parametrize("layout", DENSE_LAYOUTS)
 def test_ragged_dense_tiles(gpu, monkeypatch, layout, seg):
     """Ordered ragged layouts (the segmented-prefix path for dense tiles, the
@@ -139,7 +139,7 @@ def test_ragged_dense_tiles(gpu, monkeypatch, layout, seg):
     enough to make some tiles sparse, overlapping ordered packets, tiles
     ending exactly on a row-group boundary, 65535-B packets and empty
     packets -- every packet against the oracle.  WC_SEG: 0 = flat kernel,
-    1 = seg kernel for ip_cksum (the default), 2 = seg kernel for both kinds."""
+    1 = seg kernel (the default)."""
     monkeypatch.setenv("WC_SEG", seg)
     rng = np.random.default_rng(sum(layout.encode()))
     n = 6000
@@ -228,8 +228,13 @@ def test_empty_batch_is_noop(gpu):
 # ---------------------------------------------------------------------------
 # payload_cksum (pseudo-header) batches.
 
+SEG_MODES = ["0", "1"]  # WC_SEG: flat kernel / seg kernel (default)
+
+
+@pytest.mark.parametrize("seg", SEG_MODES)
 @pytest.mark.parametrize("align,lead", [(1, 0), (1, 3), (2, 14), (16, 14), (16, 0), (4, 1)])
-def test_payload_ragged_wild(gpu, align, lead):
+def test_payload_ragged_wild(gpu, monkeypatch, align, lead, seg):
+    monkeypatch.setenv("WC_SEG", seg)
     rng = np.random.default_rng(100 + align * 17 + lead)
     pkts = random_packets(rng, 3000, max_payload=1472, wild=True)
     buf, offs, lens = pack(pkts, align=align, lead=lead)
@@ -255,16 +260,58 @@ def test_payload_strided_netmap_layout(gpu):
         np.testing.assert_array_equal(got, want)
 
 
-def test_payload_ipv6_wrap(gpu):
+@pytest.mark.parametrize("seg", SEG_MODES)
+@pytest.mark.parametrize("align,lead", [(1, 5), (2, 0)])
+def test_payload_ipv6_wrap(gpu, monkeypatch, align, lead, seg):
+    """The reference's uint32 wrap of next_hdr << 24 (in_cksum.c:157) on
+    jumbo IPv6 packets: odd starts (the seg kernel hands such tiles to the
+    exact flat path) and even starts (the seg kernel's own exact path)."""
+    monkeypatch.setenv("WC_SEG", seg)
     rng = np.random.default_rng(8)
     pkts = [ipv6_udp(bytes([0xFF]) * p, rng, next_hdr=nh)
             for p in (60000, 65000, 65487) for nh in (17, 58, 128, 200, 255)]
-    buf, offs, lens = pack(pkts, align=1, lead=5)
+    pkts += [ipv6_udp(rng.integers(0, 256, p, dtype=np.uint8).tobytes(), rng, next_hdr=nh)
+             for p in (200, 1472, 9000) for nh in (17, 250, 253, 255)]
+    # all-0xFF bodies around the length where next_hdr 254 / 255 starts to
+    # wrap the uint32 (the seg kernel's seg_wrap_risk bound)
+    pkts += [ipv6_udp(bytes([0xFF]) * p, rng, next_hdr=nh)
+             for p in range(380, 620, 7) for nh in (254, 255)]
+    buf, offs, lens = pack(pkts, align=align, lead=lead)
     got = host(wc.cksum_ragged(dev_u8(buf, gpu), to_dev(offs, gpu), to_dev(lens, gpu),
                                kind="payload"))
     b = buf.tobytes()
     want = [py_oracle.payload_cksum(b[o:o + n], n) for o, n in zip(offs, lens)]
     np.testing.assert_array_equal(got, np.array(want, np.uint16))
+
+
+@pytest.mark.parametrize("seg", SEG_MODES)
+@pytest.mark.parametrize("align", [1, 2])
+def test_payload_malformed_headers(gpu, monkeypatch, align, seg):
+    """Random bytes as IP packets, packed: every version nibble, IHL 0..15
+    (IHL < 5 double-counts src/dst like the reference), len == hl (no
+    body), next_hdr up to 255 -- every packet against the
+    oracle, in dense tiles (seg kernel) and sparse ones."""
+    monkeypatch.setenv("WC_SEG", seg)
+    rng = np.random.default_rng(31 + align)
+    n = 4000
+    lens = rng.integers(0, 120, n).astype(np.uint16)
+    big = rng.random(n) < 0.3
+    lens[big] = rng.integers(1000, 1501, int(big.sum()))
+    pkts = []
+    for ln in lens.tolist():
+        b = bytearray(rng.integers(0, 256, 40, dtype=np.uint8).tobytes())
+        if rng.random() < 0.4:
+            b[0] = 0x40 | int(rng.integers(0, 16))
+        elif rng.random() < 0.5:
+            b[0] = 0x60 | int(rng.integers(0, 16))
+        hl = (b[0] & 15) * 4 if b[0] >> 4 == 4 else 40
+        ln = max(ln, hl)  # len < hl: the reference reads ~4 GiB (undefined)
+        body = rng.integers(0, 256, max(ln, 40) - 40, dtype=np.uint8).tobytes()
+        pkts.append((bytes(b) + body, ln))  # >= 40 bytes: the fields payload_cksum reads
+    buf, offs, lens = pack(pkts, align=align, lead=3)
+    got = host(wc.cksum_ragged(dev_u8(buf, gpu), to_dev(offs, gpu), to_dev(lens, gpu),
+                               kind="payload"))
+    np.testing.assert_array_equal(got, c_oracle.cksum_ragged(buf, offs, lens, kind=1))
 
 
 def test_verify_counts_bad_packets(gpu):

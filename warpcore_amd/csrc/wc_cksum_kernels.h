@@ -37,7 +37,8 @@
     WC_SHAPE(16, 2, 2)                                                         \
     WC_SHAPE(32, 2, 1)                                                         \
     WC_SHAPE(64, 2, 1)                                                         \
-    WC_SHAPE(64, 4, 1)
+    WC_SHAPE(64, 4, 1)                                                         \
+    WC_SHAPE(16, 6, 4)
 
 namespace wc {
 

@@ -813,15 +813,30 @@ k_cksum_flat(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
 // so the stream never touches an unmapped page.  Other tiles take the flat
 // path above.
 //
-// ip_cksum needs ONE running sum: V = sum of the little-endian words at even
+// Both kinds keep ONE running sum: V = sum of the little-endian words at even
 // addresses (v_dot2_u32_u16, 4 per chunk).  For an even-start packet V is the
 // reference's accumulator (in_cksum.c:107-120; < 2^31, no wrap).  For an odd
 // start the reference's X = O + 256 E satisfies X == 256 V == rotl32(V, 8)
 // (mod 0xFFFF, as 2^16 == 2^32 == 1) and X == 0 iff V == 0; the end-around
 // fold (in_cksum.c:74-80) maps positive numbers to [1, 0xFFFF] by their
-// residue, so fold(rotl32(V, 8)) is bit-exact.  payload_cksum adds terms that
-// can wrap the uint32 (next_hdr << 24, in_cksum.c:157), so it keeps the exact
-// byte-lane sums E and O instead (two running sums).
+// residue, so fold(rotl32(V, 8)) is bit-exact.
+//
+// payload_cksum (in_cksum.c:140-167) needs no header pass either.  Its
+// pseudo-header src/dst fields end where a standard header ends (IPv4 @12..19
+// with IHL 5, IPv6 @8..39), so body + src/dst is ONE range of the running sum,
+// [a + 12, a + len) or [a + 8, a + len).  The lone field bytes (IPv4 proto @9,
+// IPv6 payload length @4..5) come from the header load that is prefetched a
+// tile ahead anyway (load_hdr7), and an IPv4 header with options (or a
+// malformed IHL < 5) corrects the range by the bytes between byte 20 and hl,
+// from a few masked loads of those lanes alone.  Then the non-linear term
+// `special` (IPv4 plen, IPv6 next_hdr << 24) is added.  The reference adds it
+// in a uint32 that may wrap (next_hdr << 24, in_cksum.c:157).  For an even
+// start V is the exact accumulator, so V + special wraps exactly as the
+// reference does.  For an odd start the residue is exact as long as the
+// reference's sum does not wrap; a tile holding an odd-start packet that
+// could wrap (IPv6, next_hdr >= ~254 at 1500 B) takes the exact flat path
+// instead (seg_wrap_risk), as does one holding a packet shorter than its
+// header.
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
@@ -837,31 +852,49 @@ __device__ __forceinline__ uint32_t head_mask(uint32_t q, int j)
     return nb >= 4u ? 0xFFFFFFFFu : ((1u << (8u * nb)) - 1u);
 }
 
-template <int KIND>
-struct SegSum {
-    static constexpr int NV = KIND == WC_KIND_PAYLOAD ? 2 : 1;
-    uint32_t v[NV];
+// V of a chunk's first q bytes (q = 16: all of them).
+template <bool MASK>
+__device__ __forceinline__ uint32_t seg_chunk(const u32x4 &d, uint32_t q)
+{
+    uint32_t v = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        v = wsum(MASK ? pick_dword(d, j) & head_mask(q, j) : pick_dword(d, j), v);
+    return v;
+}
+
+// V of the bytes at packet offsets [lo, hi) inside a chunk that starts co
+// bytes after the packet start.
+__device__ __forceinline__ uint32_t seg_range(const u32x4 &d, int co, int lo, int hi)
+{
+    const int l = min(max(lo - co, 0), 16);
+    const int h = max(min(max(hi - co, 0), 16), l);
+    const uint32_t kb = (1u << h) - (1u << l);
+    uint32_t v = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+        v = wsum(pick_dword(d, j) & (expand_nibble(kb, j) * 0xFFu), v);
+    return v;
+}
+
+// Header bytes a payload_cksum lane needs before its tile, from ONE 16-byte
+// load at the 4-byte boundary at or below the packet start (covers packet
+// bytes 0..12, all inside the header the reference reads, in_cksum.c:142-160):
+// h0 = b0 | b2 << 8 | b3 << 16 | b6 << 24 (as load_hdr4), h1 = b4 | b5 << 8 |
+// b9 << 16.
+struct Hdr7 {
+    uint32_t h0, h1;
 };
 
-// Sum of a chunk's first q bytes (q = 16: all of them).
-template <int KIND, bool MASK>
-__device__ __forceinline__ SegSum<KIND> seg_chunk(const u32x4 &d, uint32_t q)
+__device__ __forceinline__ Hdr7 load_hdr7(uint64_t a)
 {
-    SegSum<KIND> r;
-#pragma unroll
-    for (int i = 0; i < SegSum<KIND>::NV; ++i)
-        r.v[i] = 0;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uint32_t x = MASK ? pick_dword(d, j) & head_mask(q, j) : pick_dword(d, j);
-        if constexpr (KIND == WC_KIND_PAYLOAD) {
-            r.v[0] = dot4(x, kEvenW, r.v[0]);
-            r.v[1] = dot4(x, kOddW, r.v[1]);
-        } else {
-            r.v[0] = wsum(x, r.v[0]);
-        }
-    }
-    return r;
+    const u32x4a4 d = *(const u32x4a4 __attribute__((address_space(1))) *)(uintptr_t)(a & ~3ull);
+    const uint32_t sh = 8u * (uint32_t)(a & 3u);
+    const uint32_t w0 = __builtin_amdgcn_alignbit(d.y, d.x, sh); // bytes 0..3
+    const uint32_t w1 = __builtin_amdgcn_alignbit(d.z, d.y, sh); // bytes 4..7
+    const uint32_t w2 = __builtin_amdgcn_alignbit(d.w, d.z, sh); // bytes 8..11
+    return Hdr7{__builtin_amdgcn_perm(w1, w0, 0x06030200u),
+                __builtin_amdgcn_perm(w2, w1, 0x0C050100u)};
 }
 
 template <int UNS>
@@ -882,28 +915,21 @@ __device__ __forceinline__ void seg_issue(SegRows<UNS> &R, uint64_t A0, uint32_t
 
 // Sum the UNS rows of the group at slot g0: row prefix sums (DPP), chained
 // through LDS; packet lanes whose start / end chunk falls in the group pick
-// up the running sum before it.  `carry` is the running sum before the group
-// (wave-uniform).
-template <int UNS, int KIND>
+// up the running sum before it and the chunk itself.  `carry` is the running
+// sum before the group (wave-uniform).
+template <int UNS>
 __device__ __forceinline__ void seg_accum(const SegRows<UNS> &R, uint32_t *pre, u32x4 *stage,
                                           uint32_t g0, int lane, uint32_t cs, uint32_t ce,
-                                          SegSum<KIND> &carry, SegSum<KIND> &Ps,
-                                          SegSum<KIND> &Pe, u32x4 &hs, u32x4 &he)
+                                          uint32_t &carry, uint32_t &Ps, uint32_t &Pe,
+                                          u32x4 &hs, u32x4 &he)
 {
-    constexpr int NV = SegSum<KIND>::NV;
     constexpr uint32_t kGrp = 64u * UNS;
-    uint32_t P[UNS][NV];
+    uint32_t P[UNS];
 #pragma unroll
-    for (int u = 0; u < UNS; ++u) {
-        const SegSum<KIND> c = seg_chunk<KIND, false>(R.d[u], 16u);
-#pragma unroll
-        for (int i = 0; i < NV; ++i)
-            P[u][i] = c.v[i];
-    }
+    for (int u = 0; u < UNS; ++u)
+        P[u] = seg_chunk<false>(R.d[u], 16u);
 #define WC_SEG_STEP(CTRL, ROWS)                                                \
-    _Pragma("unroll") for (int u = 0; u < UNS; ++u)                            \
-        _Pragma("unroll") for (int i = 0; i < NV; ++i)                         \
-            P[u][i] += dpp0<CTRL, ROWS>(P[u][i]);
+    _Pragma("unroll") for (int u = 0; u < UNS; ++u) P[u] += dpp0<CTRL, ROWS>(P[u]);
     WC_SEG_STEP(kDppRowShr + 1, 0xF)
     WC_SEG_STEP(kDppRowShr + 2, 0xF)
     WC_SEG_STEP(kDppRowShr + 4, 0xF)
@@ -911,19 +937,13 @@ __device__ __forceinline__ void seg_accum(const SegRows<UNS> &R, uint32_t *pre, 
     WC_SEG_STEP(kDppRowBcast15, 0xA)
     WC_SEG_STEP(kDppRowBcast31, 0xC)
 #undef WC_SEG_STEP
-    uint32_t c[NV];
-#pragma unroll
-    for (int i = 0; i < NV; ++i)
-        c[i] = carry.v[i];
+    uint32_t c = carry;
 #pragma unroll
     for (int u = 0; u < UNS; ++u) {
         stage[64u * u + lane] = R.d[u];
-#pragma unroll
-        for (int i = 0; i < NV; ++i) {
-            const uint32_t tot = __builtin_amdgcn_readlane(P[u][i], 63);
-            pre[i * kGrp + 64u * u + lane] = P[u][i] + c[i];
-            c[i] += tot;
-        }
+        const uint32_t tot = __builtin_amdgcn_readlane(P[u], 63);
+        pre[64u * u + lane] = P[u] + c;
+        c += tot;
     }
     wave_order();
     const uint32_t ds = cs - g0, de = ce - g0;
@@ -933,94 +953,113 @@ __device__ __forceinline__ void seg_accum(const SegRows<UNS> &R, uint32_t *pre, 
         hs = stage[ds];
     if (de < kGrp)
         he = stage[de];
-#pragma unroll
-    for (int i = 0; i < NV; ++i) {
-        const uint32_t vs = pre[i * kGrp + min(ds - 1u, kGrp - 1u)];
-        const uint32_t ve = pre[i * kGrp + min(de - 1u, kGrp - 1u)];
-        if (ds < kGrp)
-            Ps.v[i] = ds ? vs : carry.v[i];
-        if (de < kGrp)
-            Pe.v[i] = de ? ve : carry.v[i];
-        carry.v[i] = c[i];
-    }
+    const uint32_t vs = pre[min(ds - 1u, kGrp - 1u)];
+    const uint32_t ve = pre[min(de - 1u, kGrp - 1u)];
+    if (ds < kGrp)
+        Ps = ds ? vs : carry;
+    if (de < kGrp)
+        Pe = de ? ve : carry;
+    carry = c;
     wave_order(); // pre is rewritten by the next group
 }
 
-// One dense tile.  [a, a + len) is this lane's packet (payload: the whole IP
-// packet, header included -- the header is taken out again below, so the
-// stream never waits for the header bytes).  Returns the checksum.
+// Could the reference's uint32 sum for this odd-start payload packet wrap
+// when `special` is added?  Before it, the sum holds at most (len + 1) / 2 + 1
+// words of <= 0xFFFF (body, src/dst and proto or payload length; len >= hl),
+// so only IPv6 next_hdr >= ~254 at 1500 B (never at <= 500 B) can.
+__device__ __forceinline__ bool seg_wrap_risk(uint64_t a, uint32_t len, const PseudoHdr &ph)
+{
+    return (a & 1u) &&
+           (uint64_t)ph.special + 65535ull * ((len + 1u) / 2u + 1u) >= (1ull << 32);
+}
+
+// Can the seg path sum this payload packet?  It needs the whole header inside
+// the packet (len >= hl; the reference reads ~4 GiB otherwise) and, for IPv4,
+// the src/dst fields too.
+__device__ __forceinline__ bool seg_payload_ok(uint64_t a, uint32_t len, const PseudoHdr &ph)
+{
+    return len >= max(ph.hl, 20u) && !seg_wrap_risk(a, len, ph);
+}
+
+// One dense tile.  [a, a + len) is this lane's packet; ip_cksum sums all of
+// it, payload_cksum the range [a + f1, a + len) plus the corrections above.
+// Returns the checksum.
 template <int UNS, int KIND, bool NT, class F>
 __device__ __forceinline__ uint16_t seg_tile(uint32_t *pre, u32x4 *stage, int lane, uint64_t a,
-                                             uint32_t len,
-                                             const PseudoHdr &ph, uint64_t A0, uint32_t T,
-                                             uint64_t zero, F &&after_first_issue)
+                                             uint32_t len, const PseudoHdr &ph, uint32_t h1,
+                                             uint64_t A0, uint32_t T, uint64_t zero,
+                                             F &&after_first_issue)
 {
-    constexpr int NV = SegSum<KIND>::NV;
     constexpr uint32_t kGrp = 64u * UNS;
-    const uint64_t rs = a - A0, re = rs + len;
+    constexpr bool PL = KIND == WC_KIND_PAYLOAD;
+    const uint32_t f1 = PL ? (ph.v4 ? 12u : 8u) : 0u;
+    const uint64_t rs = a + f1 - A0, re = a + len - A0;
     const uint32_t cs = (uint32_t)(rs >> 4), qs = (uint32_t)(rs & 15u);
     const uint32_t ce = (uint32_t)(re >> 4), qe = (uint32_t)(re & 15u);
 
     SegRows<UNS> A, B;
     seg_issue<UNS, NT>(A, A0, 0, lane, T, zero);
     after_first_issue();
-    // For payload_cksum: the packet's header chunks.
-    u32x4 hs = {0u, 0u, 0u, 0u}, he = {0u, 0u, 0u, 0u};
-    constexpr int NH = KIND == WC_KIND_PAYLOAD ? 5 : 0; // [0, 60) from any phase
-    u32x4 hc[NH > 0 ? NH : 1];
-    const uint32_t s = (uint32_t)(a & 15u);
-    if constexpr (NH > 0) {
-        const uint32_t nspan = (s + max(len, 20u) + 15u) >> 4;
+    // payload_cksum, IPv4 with hl != 20: the bytes between 20 and hl (<= 40
+    // bytes, <= 4 chunks), loaded by those lanes alone.
+    u32x4 xc[PL ? 4 : 1];
+    const bool corr = PL && ph.v4 && ph.hl != 20u;
+    const int clo = (int)min(ph.hl, 20u), chi = (int)max(ph.hl, 20u);
+    const uint64_t ca = (a + (uint32_t)clo) & ~15ull;
+    if constexpr (PL) {
 #pragma unroll
-        for (int k = 0; k < NH; ++k)
-            hc[k] = load_chunk<false>((uint32_t)k < nspan ? (a & ~15ull) + 16ull * k : zero);
+        for (int k = 0; k < 4; ++k)
+            xc[k] = u32x4{0u, 0u, 0u, 0u};
+        if (corr) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (ca + 16ull * k < a + (uint32_t)chi)
+                    xc[k] = load_chunk<false>(ca + 16ull * k);
+        }
     }
 
-    SegSum<KIND> carry, Ps, Pe;
-#pragma unroll
-    for (int i = 0; i < NV; ++i)
-        carry.v[i] = Ps.v[i] = Pe.v[i] = 0;
+    uint32_t carry = 0, Ps = 0, Pe = 0;
+    u32x4 hs = {0u, 0u, 0u, 0u}, he = {0u, 0u, 0u, 0u};
     uint32_t j = 0;
     for (; j < T; j += 2 * kGrp) {
         seg_issue<UNS, NT>(B, A0, j + kGrp, lane, T, zero);
         __builtin_amdgcn_sched_barrier(0);
-        seg_accum<UNS, KIND>(A, pre, stage, j, lane, cs, ce, carry, Ps, Pe, hs, he);
+        seg_accum<UNS>(A, pre, stage, j, lane, cs, ce, carry, Ps, Pe, hs, he);
         __builtin_amdgcn_sched_barrier(0);
         seg_issue<UNS, NT>(A, A0, j + 2 * kGrp, lane, T, zero);
         __builtin_amdgcn_sched_barrier(0);
-        seg_accum<UNS, KIND>(B, pre, stage, j + kGrp, lane, cs, ce, carry, Ps, Pe, hs, he);
+        seg_accum<UNS>(B, pre, stage, j + kGrp, lane, cs, ce, carry, Ps, Pe, hs, he);
         __builtin_amdgcn_sched_barrier(0);
     }
     if (ce >= j) // the packet ends exactly at the last row group's end
-#pragma unroll
-        for (int i = 0; i < NV; ++i)
-            Pe.v[i] = carry.v[i];
+        Pe = carry;
 
-    const SegSum<KIND> ps = seg_chunk<KIND, true>(hs, qs);
-    const SegSum<KIND> pe = seg_chunk<KIND, true>(he, qe);
-    uint32_t v[NV];
+    uint32_t v = (Pe + seg_chunk<true>(he, qe)) - (Ps + seg_chunk<true>(hs, qs));
+    if constexpr (PL) {
+        // Lone field bytes at their address weight: IPv4 proto @9 (odd
+        // offset), IPv6 payload length @4..5 (a word at an even offset).
+        const uint32_t odd = (uint32_t)(a & 1u);
+        const uint32_t b9 = (h1 >> 16) & 0xFFu, b4 = h1 & 0xFFu, b5 = (h1 >> 8) & 0xFFu;
+        v += ph.v4 ? (odd ? b9 : b9 << 8) : (odd ? (b4 << 8) | b5 : b4 | (b5 << 8));
+        if (corr) {
+            // hl < 20: the body starts early (src/dst count twice, as in the
+            // reference); hl > 20: the options are not summed.
+            uint32_t cv = 0;
 #pragma unroll
-    for (int i = 0; i < NV; ++i)
-        v[i] = (Pe.v[i] + pe.v[i]) - (Ps.v[i] + ps.v[i]);
-    if constexpr (KIND == WC_KIND_PAYLOAD) {
-        // payload = packet - header [0, hl) + pseudo-header fields (whose
-        // bytes inside the header thus count once, outside it twice -- the
-        // reference's own result for a malformed IHL < 5).  len < hl (no
-        // payload; the reference would read 4 GiB): fields only, as the flat
-        // path computes it.
-        uint32_t Ef = 0, Of = 0, Eh = 0, Oh = 0;
-#pragma unroll
-        for (int k = 0; k < NH; ++k) {
-            const int co = 16 * k - (int)s;
-            accum_arith<WC_KIND_PAYLOAD>(hc[k], co, 0, 0, ph.v4, Ef, Of);
-            accum_arith<WC_KIND_IP>(hc[k], co, 0, (int)ph.hl, 0u, Eh, Oh);
+            for (int k = 0; k < 4; ++k)
+                cv += seg_range(xc[k], (int)(ca - a) + 16 * k, clo, chi);
+            v = ph.hl < 20u ? v + cv : v - cv;
         }
-        const bool body = len >= ph.hl;
-        const uint32_t E = (body ? v[0] - Eh : 0u) + Ef;
-        const uint32_t O = (body ? v[1] - Oh : 0u) + Of;
-        return fold_not(combine(E, O, a & 1u) + ph.special);
+    }
+    if (!(a & 1u))
+        return fold_not(v + ph.special); // exact, wrap included
+    const uint32_t r8 = __builtin_amdgcn_alignbit(v, v, 24); // rotl32(v, 8)
+    if constexpr (PL) {
+        // residue of r8 + special (no wrap: seg_wrap_risk), zero iff both are
+        const uint64_t t = (uint64_t)r8 + ph.special;
+        return fold_not((uint32_t)(t & 0xFFFFu) + (uint32_t)(t >> 16));
     } else {
-        return fold_not((a & 1u) ? __builtin_amdgcn_alignbit(v[0], v[0], 24) : v[0]);
+        return fold_not(r8);
     }
 }
 
@@ -1054,14 +1093,14 @@ template <int UN, int UNS, int KIND, bool NT>
 __global__ void __launch_bounds__(256)
 k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
             const uint16_t *__restrict__ lens, uint64_t n, uint16_t *__restrict__ out,
-            unsigned long long *__restrict__ bad)
+            unsigned long long *__restrict__ bad, int variant)
 {
-    constexpr int NV = SegSum<KIND>::NV;
+    (void)variant; // WC_VARIANT: A/B experiments
     union TileLds {
         FlatLds<UN> flat;
         struct {
             u32x4 stage[64 * UNS]; // the row group's chunks
-            uint32_t pre[NV * 64 * UNS];
+            uint32_t pre[64 * UNS];
         } seg;
     };
     __shared__ TileLds lds_all[kFlatWaves];
@@ -1078,9 +1117,10 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     uint64_t p = tile * 64 + lane;
     uint64_t off_n = p < n ? offs[p] : 0;
     uint32_t len_n = p < n ? (uint32_t)lens[p] : 0u;
-    uint32_t hdr_n = 0;
+    Hdr7 hdr_n{0u, 0u};
     if constexpr (KIND == WC_KIND_PAYLOAD)
-        hdr_n = p < n ? load_hdr4((uint64_t)base + off_n) : 0u;
+        if (p < n)
+            hdr_n = load_hdr7((uint64_t)base + off_n);
 
     for (; tile < ntiles; tile += nwaves) {
         p = tile * 64 + lane;
@@ -1088,28 +1128,32 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
         const uint32_t nvalid = (uint32_t)min<uint64_t>(64, n - tile * 64);
         const uint64_t off = off_n;
         const uint32_t len = len_n;
-        const uint32_t hdr4 = hdr_n;
+        const Hdr7 hdr = hdr_n;
         const uint64_t pn = (tile + nwaves) * 64 + lane;
         const bool valid_n = pn < n;
         off_n = valid_n ? offs[pn] : 0;
         len_n = valid_n ? (uint32_t)lens[pn] : 0u;
         auto prefetch_hdr = [&] {
             if constexpr (KIND == WC_KIND_PAYLOAD)
-                hdr_n = valid_n ? load_hdr4((uint64_t)base + off_n) : 0u;
+                if (valid_n)
+                    hdr_n = load_hdr7((uint64_t)base + off_n);
         };
 
         const uint64_t a = (uint64_t)base + off;
         PseudoHdr ph{0u, 1u, 0u};
         if constexpr (KIND == WC_KIND_PAYLOAD)
             if (valid)
-                ph = pseudo_hdr(hdr4 & 0xFFu, (hdr4 >> 8) & 0xFFu, (hdr4 >> 16) & 0xFFu,
-                                hdr4 >> 24);
+                ph = pseudo_hdr(hdr.h0 & 0xFFu, (hdr.h0 >> 8) & 0xFFu, (hdr.h0 >> 16) & 0xFFu,
+                                hdr.h0 >> 24);
         uint64_t A0 = 0;
         uint32_t T = 0;
         uint16_t r;
-        if (seg_dense(lane, a, len, valid, nvalid, A0, T))
-            r = seg_tile<UNS, KIND, NT>(L.seg.pre, L.seg.stage, lane, a, len, ph, A0, T, zero,
-                                        prefetch_hdr);
+        bool dense = seg_dense(lane, a, len, valid, nvalid, A0, T);
+        if constexpr (KIND == WC_KIND_PAYLOAD)
+            dense = dense && !__ballot(valid && !seg_payload_ok(a, len, ph));
+        if (dense)
+            r = seg_tile<UNS, KIND, NT>(L.seg.pre, L.seg.stage, lane, a, len, ph, hdr.h1, A0, T,
+                                        zero, prefetch_hdr);
         else
             r = fold_not(flat_tile_sum<UN, KIND, NT, false, true>(L.flat, nullptr, lane, a, len,
                                                                   valid, ph, prefetch_hdr));
@@ -1240,10 +1284,10 @@ static hipError_t launch_flat_un(const LaunchArgs &a, hipStream_t st)
 #define WC_SEG(US)                                                             \
     if (a.kind == WC_KIND_PAYLOAD)                                             \
         hipLaunchKernelGGL((k_cksum_seg<UN, US, WC_KIND_PAYLOAD, true>), dim3(grid), \
-                           dim3(256), 0, st, b, a.offs, a.lens, a.n, a.out, bad); \
+                           dim3(256), 0, st, b, a.offs, a.lens, a.n, a.out, bad, a.variant); \
     else                                                                       \
         hipLaunchKernelGGL((k_cksum_seg<UN, US, WC_KIND_IP, true>), dim3(grid), \
-                           dim3(256), 0, st, b, a.offs, a.lens, a.n, a.out, bad);
+                           dim3(256), 0, st, b, a.offs, a.lens, a.n, a.out, bad, a.variant);
         if (a.seg_rows == 2) {
             WC_SEG(2)
         } else if (a.seg_rows == 8) {
