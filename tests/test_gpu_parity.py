@@ -39,6 +39,24 @@ def host(t: torch.Tensor) -> np.ndarray:
     return t.cpu().numpy().view(np.uint16)
 
 
+# Ragged kernel paths (wc_cksum_api.cpp plan_ragged, k_cksum_seg): the flat
+# kernel alone; the seg kernel without its grouped path; the grouped path
+# forced for every tile; and the default per-tile choice.
+RAGGED_MODES = {
+    "flat": {"WC_SEG": "0"},
+    "seg": {"WC_SEG": "1", "WC_GRP_DENSE": "65", "WC_GRP_SPARSE": "65"},
+    "grp": {"WC_SEG": "1", "WC_GRP_DENSE": "0", "WC_GRP_SPARSE": "0"},
+    "default": {},
+}
+
+
+def ragged_mode(monkeypatch, mode: str) -> None:
+    for k in ("WC_SEG", "WC_GRP_DENSE", "WC_GRP_SPARSE"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in RAGGED_MODES[mode].items():
+        monkeypatch.setenv(k, v)
+
+
 # ---------------------------------------------------------------------------
 # Known answers and golden vectors.
 
@@ -102,7 +120,9 @@ def test_strided_sweep(gpu, length):
             np.testing.assert_array_equal(got, want, err_msg=f"stride {stride} start {start}")
 
 
-def test_ragged_random_placement(gpu):
+@pytest.mark.parametrize("mode", list(RAGGED_MODES))
+def test_ragged_random_placement(gpu, monkeypatch, mode):
+    ragged_mode(monkeypatch, mode)
     rng = np.random.default_rng(11)
     buf = rng.integers(0, 256, 1 << 20, dtype=np.uint8)
     n = 20000
@@ -131,16 +151,15 @@ DENSE_LAYOUTS = ["packed", "packed_tiny", "gaps", "gaps_wide", "overlap", "exact
                  "jumbo", "with_empty"]
 
 
-@pytest.mark.parametrize("seg", ["0", "1"])
+@pytest.mark.parametrize("mode", list(RAGGED_MODES))
 @pytest.mark.parametrize("layout", DENSE_LAYOUTS)
-def test_ragged_dense_tiles(gpu, monkeypatch, layout, seg):
+def test_ragged_dense_tiles(gpu, monkeypatch, layout, mode):
     """Ordered ragged layouts (the segmented-prefix path for dense tiles, the
     flat path for the rest): packed at every alignment, small gaps, gaps wide
     enough to make some tiles sparse, overlapping ordered packets, tiles
     ending exactly on a row-group boundary, 65535-B packets and empty
-    packets -- every packet against the oracle.  WC_SEG: 0 = flat kernel,
-    1 = seg kernel (the default)."""
-    monkeypatch.setenv("WC_SEG", seg)
+    packets -- every packet against the oracle, on every ragged path."""
+    ragged_mode(monkeypatch, mode)
     rng = np.random.default_rng(sum(layout.encode()))
     n = 6000
     lens = rng.integers(1, 2001, n).astype(np.uint16)
@@ -212,6 +231,57 @@ def test_ragged_group_kernel(gpu, monkeypatch, shape):
     np.testing.assert_array_equal(got, c_oracle.cksum_ragged(buf, offs, lens, kind=1))
 
 
+@pytest.mark.parametrize("mode", list(RAGGED_MODES))
+@pytest.mark.parametrize("kind", ["ip", "payload"])
+@pytest.mark.parametrize("shape", ["slots", "slots_jitter", "uniform_packed", "jumbo", "tail"])
+def test_ragged_uniform_tiles(gpu, monkeypatch, kind, shape, mode):
+    """Uniform-length ragged batches (the grouped path's tiles): a netmap RX
+    ring drained into one batch -- 2048-B slots, IP packet at +14
+    (backend_netmap.c:379-391, eth.h:44-48) with exact and jittered lengths,
+    v4 / v6 mixed -- packed equal packets at odd alignment, 9000-B jumbo
+    frames, and a batch whose last tile is partial.  Every packet against
+    the oracle."""
+    ragged_mode(monkeypatch, mode)
+    rng = np.random.default_rng(sum(shape.encode()) + (kind == "payload"))
+    n, slot, at = 3000, 2048, 14
+    if shape == "slots":
+        lens = np.full(n, 1500, np.int64)
+    elif shape == "slots_jitter":
+        lens = rng.integers(1300, 1501, n)
+    elif shape == "uniform_packed":
+        lens = np.full(n, 1001, np.int64)
+    elif shape == "jumbo":
+        n, slot = 400, 9216
+        lens = rng.integers(8900, 9001, n)
+    else:  # tail: 64 k + 5 packets
+        n = 64 * 7 + 5
+        lens = rng.integers(1400, 1501, n)
+    if shape == "uniform_packed":
+        offs = 3 + np.arange(n, dtype=np.uint64) * 1001
+        size = int(offs[-1]) + 1001 + 64
+    else:
+        offs = np.arange(n, dtype=np.uint64) * slot + at
+        size = n * slot + 64
+    buf = rng.integers(0, 256, size, dtype=np.uint8)
+    if kind == "payload":
+        for i, (o, ln) in enumerate(zip(offs.tolist(), lens.tolist())):
+            payload = rng.integers(0, 256, ln - 28 - (20 if i % 3 == 0 else 0),
+                                   dtype=np.uint8).tobytes()
+            pkt, plen = (ipv6_udp if i % 3 == 0 else ipv4_udp)(payload, rng)
+            assert plen == ln == len(pkt)
+            buf[o:o + ln] = np.frombuffer(pkt, np.uint8)
+    lens = lens.astype(np.uint16)
+    k = 1 if kind == "payload" else 0
+    got = host(wc.cksum_ragged(dev_u8(buf, gpu), to_dev(offs, gpu), to_dev(lens, gpu), kind=k))
+    np.testing.assert_array_equal(got, c_oracle.cksum_ragged(buf, offs, lens, kind=k))
+    if kind == "payload":  # RX verify of the same ring after the TX pass stored them
+        for i, (o, ln) in enumerate(zip(offs.tolist(), lens.tolist())):
+            pkt = insert_checksum(bytes(buf[o:o + ln]), int(got[i]))
+            buf[o:o + ln] = np.frombuffer(pkt, np.uint8)
+        v = host(wc.cksum_ragged(dev_u8(buf, gpu), to_dev(offs, gpu), to_dev(lens, gpu), kind=1))
+        assert (v == 0).all()
+
+
 def test_all_zero_and_all_ones(gpu):
     for fill, want in ((0x00, 0xFFFF), (0xFF, 0x0000)):
         buf = np.full(1472 * 64, fill, dtype=np.uint8)
@@ -228,13 +298,10 @@ def test_empty_batch_is_noop(gpu):
 # ---------------------------------------------------------------------------
 # payload_cksum (pseudo-header) batches.
 
-SEG_MODES = ["0", "1"]  # WC_SEG: flat kernel / seg kernel (default)
-
-
-@pytest.mark.parametrize("seg", SEG_MODES)
+@pytest.mark.parametrize("mode", list(RAGGED_MODES))
 @pytest.mark.parametrize("align,lead", [(1, 0), (1, 3), (2, 14), (16, 14), (16, 0), (4, 1)])
-def test_payload_ragged_wild(gpu, monkeypatch, align, lead, seg):
-    monkeypatch.setenv("WC_SEG", seg)
+def test_payload_ragged_wild(gpu, monkeypatch, align, lead, mode):
+    ragged_mode(monkeypatch, mode)
     rng = np.random.default_rng(100 + align * 17 + lead)
     pkts = random_packets(rng, 3000, max_payload=1472, wild=True)
     buf, offs, lens = pack(pkts, align=align, lead=lead)
@@ -260,13 +327,13 @@ def test_payload_strided_netmap_layout(gpu):
         np.testing.assert_array_equal(got, want)
 
 
-@pytest.mark.parametrize("seg", SEG_MODES)
+@pytest.mark.parametrize("mode", list(RAGGED_MODES))
 @pytest.mark.parametrize("align,lead", [(1, 5), (2, 0)])
-def test_payload_ipv6_wrap(gpu, monkeypatch, align, lead, seg):
+def test_payload_ipv6_wrap(gpu, monkeypatch, align, lead, mode):
     """The reference's uint32 wrap of next_hdr << 24 (in_cksum.c:157) on
     jumbo IPv6 packets: odd starts (the seg kernel hands such tiles to the
     exact flat path) and even starts (the seg kernel's own exact path)."""
-    monkeypatch.setenv("WC_SEG", seg)
+    ragged_mode(monkeypatch, mode)
     rng = np.random.default_rng(8)
     pkts = [ipv6_udp(bytes([0xFF]) * p, rng, next_hdr=nh)
             for p in (60000, 65000, 65487) for nh in (17, 58, 128, 200, 255)]
@@ -284,14 +351,14 @@ def test_payload_ipv6_wrap(gpu, monkeypatch, align, lead, seg):
     np.testing.assert_array_equal(got, np.array(want, np.uint16))
 
 
-@pytest.mark.parametrize("seg", SEG_MODES)
+@pytest.mark.parametrize("mode", list(RAGGED_MODES))
 @pytest.mark.parametrize("align", [1, 2])
-def test_payload_malformed_headers(gpu, monkeypatch, align, seg):
+def test_payload_malformed_headers(gpu, monkeypatch, align, mode):
     """Random bytes as IP packets, packed: every version nibble, IHL 0..15
     (IHL < 5 double-counts src/dst like the reference), len == hl (no
     body), next_hdr up to 255 -- every packet against the
     oracle, in dense tiles (seg kernel) and sparse ones."""
-    monkeypatch.setenv("WC_SEG", seg)
+    ragged_mode(monkeypatch, mode)
     rng = np.random.default_rng(31 + align)
     n = 4000
     lens = rng.integers(0, 120, n).astype(np.uint16)
@@ -367,10 +434,10 @@ def test_c3_mtu_sweep_full(gpu, L):
     np.testing.assert_array_equal(got, c_oracle.cksum_strided(hb, L, L, n, kind=0))
 
 
-@pytest.mark.parametrize("seg", ["1", "0"])
-def test_c4_zipf_full(gpu, monkeypatch, seg):
+@pytest.mark.parametrize("mode", ["default", "flat"])
+def test_c4_zipf_full(gpu, monkeypatch, mode):
     """C4 in full through the seg kernel (default) and the flat kernel."""
-    monkeypatch.setenv("WC_SEG", seg)
+    ragged_mode(monkeypatch, mode)
     lens = synth.zipf_lengths(1 << 24)
     offs = synth.packed_offsets(lens)
     total = int(offs[-1]) + int(lens[-1])

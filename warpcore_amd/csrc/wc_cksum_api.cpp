@@ -284,6 +284,8 @@ int run(const Device &D, const wc::LaunchArgs &args, const Plan &p, hipStream_t 
     (void)D;
     wc::LaunchArgs a = args;
     a.seg_rows = p.seg_rows;
+    a.grp_thr = env_int("WC_GRP_DENSE", 65) | (env_int("WC_GRP_SPARSE", 40) << 8);
+    a.grp_rows = env_int("WC_GRP_ROWS", 4);
     hipError_t e = p.shape.group == 0 ? wc::launch_flat(a, p.shape.unroll, st)
                                       : wc::launch_cksum(a, p.shape, p.grid, st);
     return hip_err(e);

@@ -60,6 +60,10 @@ struct LaunchArgs {
     bool diag_noload;   // WC_DIAG_NOLOAD=1: timing-only flat build (wrong results)
     int variant = 0;    // WC_VARIANT: experimental kernel variants (A/B tuning)
     int seg_rows = 0;   // ragged: 0 = flat kernel, else k_cksum_seg with 2/4/8-row groups
+    // k_cksum_seg: minimum chunk fill (in 64ths) for a tile's grouped path,
+    // dense tiles | sparse tiles << 8 (65 = never)
+    int grp_thr = 65 | (40 << 8);
+    int grp_rows = 4; // k_cksum_seg grouped path: rows per ping-pong group (2, 4)
 };
 
 struct Shape {

@@ -507,6 +507,39 @@ __device__ __forceinline__ uint32_t mbcnt64(uint64_t m)
                                      __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+// Wave-uniform broadcasts and shifts without LDS round trips (readlane /
+// DPP instead of ds_bpermute).
+__device__ __forceinline__ uint32_t lane_u32(uint32_t v, int l)
+{
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+
+__device__ __forceinline__ uint64_t lane_u64(uint64_t v, int l)
+{
+    return (uint64_t)lane_u32((uint32_t)v, l) | ((uint64_t)lane_u32((uint32_t)(v >> 32), l) << 32);
+}
+
+constexpr int kDppWaveShr1 = 0x138;
+
+// v of lane - 1 (0 in lane 0).
+__device__ __forceinline__ uint64_t wave_shr1_u64(uint64_t v)
+{
+    return (uint64_t)dpp0<kDppWaveShr1, 0xF>((uint32_t)v) |
+           ((uint64_t)dpp0<kDppWaveShr1, 0xF>((uint32_t)(v >> 32)) << 32);
+}
+
+// Wave maximum (DPP max-scan; lane 63 holds the result).
+__device__ __forceinline__ uint32_t wave_max(uint32_t v)
+{
+    v = max(v, dpp0<kDppRowShr + 1, 0xF>(v));
+    v = max(v, dpp0<kDppRowShr + 2, 0xF>(v));
+    v = max(v, dpp0<kDppRowShr + 4, 0xF>(v));
+    v = max(v, dpp0<kDppRowShr + 8, 0xF>(v));
+    v = max(v, dpp0<kDppRowBcast15, 0xA>(v));
+    v = max(v, dpp0<kDppRowBcast31, 0xC>(v));
+    return lane_u32(v, 63);
+}
+
 struct FlatDesc {          // 16 bytes per non-empty packet of the tile, in LDS
     uint32_t vb_lo, vb_hi; // chunk q of the packet sits at vb + 16 q
     uint32_t rel;          // packet start in the tile's slot-byte space
@@ -682,7 +715,7 @@ __device__ __forceinline__ uint32_t flat_tile_sum(FlatLds<UN> &L, const WeightLu
     // rank among the tile's non-empty packets.
     const uint32_t ce = wave_incl_sum(nch);
     const uint32_t cp = ce - nch;
-    const uint32_t total = __shfl(ce, 63, 64);
+    const uint32_t total = lane_u32(ce, 63);
     const uint64_t nonempty = __ballot(nch != 0);
     const uint32_t rank = mbcnt64(nonempty);
     const uint32_t last_rank = nonempty ? (uint32_t)__builtin_popcountll(nonempty) - 1u : 0u;
@@ -997,26 +1030,29 @@ __device__ __forceinline__ uint16_t seg_tile(uint32_t *pre, u32x4 *stage, int la
     const uint32_t cs = (uint32_t)(rs >> 4), qs = (uint32_t)(rs & 15u);
     const uint32_t ce = (uint32_t)(re >> 4), qe = (uint32_t)(re & 15u);
 
+    // payload_cksum, IPv4 with hl != 20: V of the bytes between 20 and hl
+    // (<= 40 bytes, <= 4 chunks), loaded by those lanes alone and summed
+    // before the stream starts, so the chunks hold no registers across it.
+    const bool corr = PL && ph.v4 && ph.hl != 20u;
+    uint32_t cv = 0;
+    if constexpr (PL) {
+        if (__ballot(corr)) {
+            const int clo = (int)min(ph.hl, 20u), chi = (int)max(ph.hl, 20u);
+            const uint64_t ca = (a + (uint32_t)clo) & ~15ull;
+            u32x4 xc[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                xc[k] = load_chunk<false>(corr && ca + 16ull * k < a + (uint32_t)chi
+                                              ? ca + 16ull * k : zero);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                cv += seg_range(xc[k], (int)(ca - a) + 16 * k, clo, chi);
+        }
+    }
+
     SegRows<UNS> A, B;
     seg_issue<UNS, NT>(A, A0, 0, lane, T, zero);
     after_first_issue();
-    // payload_cksum, IPv4 with hl != 20: the bytes between 20 and hl (<= 40
-    // bytes, <= 4 chunks), loaded by those lanes alone.
-    u32x4 xc[PL ? 4 : 1];
-    const bool corr = PL && ph.v4 && ph.hl != 20u;
-    const int clo = (int)min(ph.hl, 20u), chi = (int)max(ph.hl, 20u);
-    const uint64_t ca = (a + (uint32_t)clo) & ~15ull;
-    if constexpr (PL) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-            xc[k] = u32x4{0u, 0u, 0u, 0u};
-        if (corr) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (ca + 16ull * k < a + (uint32_t)chi)
-                    xc[k] = load_chunk<false>(ca + 16ull * k);
-        }
-    }
 
     uint32_t carry = 0, Ps = 0, Pe = 0;
     u32x4 hs = {0u, 0u, 0u, 0u}, he = {0u, 0u, 0u, 0u};
@@ -1041,15 +1077,10 @@ __device__ __forceinline__ uint16_t seg_tile(uint32_t *pre, u32x4 *stage, int la
         const uint32_t odd = (uint32_t)(a & 1u);
         const uint32_t b9 = (h1 >> 16) & 0xFFu, b4 = h1 & 0xFFu, b5 = (h1 >> 8) & 0xFFu;
         v += ph.v4 ? (odd ? b9 : b9 << 8) : (odd ? (b4 << 8) | b5 : b4 | (b5 << 8));
-        if (corr) {
-            // hl < 20: the body starts early (src/dst count twice, as in the
-            // reference); hl > 20: the options are not summed.
-            uint32_t cv = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                cv += seg_range(xc[k], (int)(ca - a) + 16 * k, clo, chi);
+        // hl < 20: the body starts early (src/dst count twice, as in the
+        // reference); hl > 20: the options are not summed.
+        if (corr)
             v = ph.hl < 20u ? v + cv : v - cv;
-        }
     }
     if (!(a & 1u))
         return fold_not(v + ph.special); // exact, wrap included
@@ -1063,6 +1094,153 @@ __device__ __forceinline__ uint16_t seg_tile(uint32_t *pre, u32x4 *stage, int la
     }
 }
 
+// ---------------------------------------------------------------------------
+// Ragged batches, uniform tiles: the "grouped" path.
+//
+// When a tile's packets have similar chunk counts (a netmap RX ring: fixed
+// 2048-B slots holding ~MTU packets at +14, backend_netmap.c:379-391), the
+// wave sums it the way the strided kernel sums a batch: 16 lanes per packet,
+// four packets per 64-chunk row, R = ceil(max chunks / 16) rows per quad of
+// packets, 16 quads per tile.  A chunk's address is its packet's base + 16 c
+// -- no owner lookup, no scan, no LDS per row -- and the lanes keep exact
+// byte-lane sums (E, O), so payload_cksum needs no wrap guard.  Slots past a
+// packet's end read the zero chunk.  A quad's 16 lane sums are reduced with
+// a DPP row scan and its four results parked in LDS until the tile's packet
+// lanes store them.  Used when the tile's chunks fill at least thr / 64 of
+// its 1024 R slots (LaunchArgs::grp_thr): sparse tiles from 40/64 on (netmap
+// slots: 71 -> 78 % of HBM peak); dense tiles stay on the seg path, which
+// measured faster on them (rc2: 84.7 vs 82.2 %).
+
+struct GrpDesc { // one per packet of the tile, in LDS
+    uint32_t a_lo, a_hi;
+    uint32_t info; // len | hl << 16 | v4 << 24
+    uint32_t special;
+};
+
+struct GrpLds {
+    GrpDesc gd[64];
+    uint32_t res[64];
+};
+
+// Issue-side walk state: quad q, row k within it, and the quad's descriptor
+// as this lane sees it (its packet = 4 q + lane / 16).
+struct GrpIssue {
+    uint32_t q, k;
+    uint64_t cb;  // packet's first aligned chunk
+    uint32_t nch; // its chunk count
+};
+
+template <int UNG>
+struct GrpRows {
+    u32x4 d[UNG];
+};
+
+__device__ __forceinline__ void grp_load_quad(GrpIssue &I, const GrpLds &L, int lane)
+{
+    const GrpDesc g = L.gd[min(4u * I.q + ((uint32_t)lane >> 4), 63u)];
+    const uint64_t a = (uint64_t)g.a_lo | ((uint64_t)g.a_hi << 32);
+    const uint32_t len = g.info & 0xFFFFu;
+    I.cb = a & ~15ull;
+    I.nch = I.q < 16u && len ? (uint32_t)((a & 15u) + len + 15u) >> 4 : 0u;
+}
+
+template <int UNG, bool NT>
+__device__ __forceinline__ void grp_issue(GrpRows<UNG> &R, GrpIssue &I, const GrpLds &L,
+                                          int lane, uint32_t Rq, uint64_t zero)
+{
+#pragma unroll
+    for (int u = 0; u < UNG; ++u) {
+        const uint32_t c = 16u * I.k + ((uint32_t)lane & 15u);
+        R.d[u] = load_chunk<NT>(c < I.nch ? I.cb + 16ull * c : zero);
+        if (++I.k == Rq) { // wave-uniform
+            I.k = 0;
+            ++I.q;
+            grp_load_quad(I, L, lane);
+        }
+    }
+}
+
+// Accumulate-side walk state.
+struct GrpAcc {
+    uint32_t q, k;
+    uint32_t s, len, hl, v4, special;
+    uint32_t E, O;
+};
+
+__device__ __forceinline__ void grp_acc_quad(GrpAcc &S, const GrpLds &L, int lane)
+{
+    const GrpDesc g = L.gd[min(4u * S.q + ((uint32_t)lane >> 4), 63u)];
+    S.s = g.a_lo & 15u;
+    S.len = S.q < 16u ? g.info & 0xFFFFu : 0u;
+    S.hl = (g.info >> 16) & 0xFFu;
+    S.v4 = (g.info >> 24) & 1u;
+    S.special = g.special;
+}
+
+template <int UNG, int KIND>
+__device__ __forceinline__ void grp_accum(const GrpRows<UNG> &R, GrpAcc &S, GrpLds &L, int lane,
+                                          uint32_t Rq)
+{
+    const uint32_t gl = (uint32_t)lane & 15u;
+#pragma unroll
+    for (int u = 0; u < UNG; ++u) {
+        if (S.q < 16u) { // wave-uniform: rows past the tile's last quad are idle
+            const uint32_t c = 16u * S.k + gl;
+            const uint32_t nch = S.len ? (S.s + S.len + 15u) >> 4 : 0u;
+            uint32_t eh = 0, oh = 0;
+            accum_strided<KIND, false, false>(R.d[u], 16 * (int)c - (int)S.s,
+                                              KIND == WC_KIND_PAYLOAD ? (int)S.hl : 0,
+                                              (int)S.len, c < nch, S.v4, S.E, S.O, eh, oh);
+            if (++S.k == Rq) {
+                // Quad done: exact reference accumulator of each packet
+                // (in_cksum.c:140-167 / 107-120, mod 2^32), row scan to lane 15.
+                uint32_t x = combine(S.E, S.O, S.s & 1u) + (gl == 0 ? S.special : 0u);
+                x += dpp0<kDppRowShr + 1, 0xF>(x);
+                x += dpp0<kDppRowShr + 2, 0xF>(x);
+                x += dpp0<kDppRowShr + 4, 0xF>(x);
+                x += dpp0<kDppRowShr + 8, 0xF>(x);
+                if (gl == 15u)
+                    L.res[4u * S.q + ((uint32_t)lane >> 4)] = fold_not(x);
+                S.E = S.O = 0u;
+                S.k = 0;
+                ++S.q;
+                grp_acc_quad(S, L, lane);
+            }
+        }
+    }
+}
+
+// One uniform tile.  Returns this lane's packet's checksum.
+template <int UNG, int KIND, bool NT, class F>
+__device__ __forceinline__ uint16_t grp_tile(GrpLds &L, int lane, uint64_t a, uint32_t len,
+                                             bool valid, const PseudoHdr &ph, uint32_t Rq,
+                                             uint64_t zero, F &&after_first_issue)
+{
+    L.gd[lane] = GrpDesc{(uint32_t)a, (uint32_t)(a >> 32),
+                         (valid ? len : 0u) | (ph.hl << 16) | (ph.v4 << 24), ph.special};
+    wave_order();
+    GrpIssue I{0u, 0u, 0ull, 0u};
+    grp_load_quad(I, L, lane);
+    GrpAcc S{};
+    grp_acc_quad(S, L, lane);
+    const uint32_t rows = 16u * Rq;
+    GrpRows<UNG> A, B;
+    grp_issue<UNG, NT>(A, I, L, lane, Rq, zero);
+    after_first_issue();
+    for (uint32_t j = 0; j < rows; j += 2u * UNG) {
+        grp_issue<UNG, NT>(B, I, L, lane, Rq, zero);
+        __builtin_amdgcn_sched_barrier(0);
+        grp_accum<UNG, KIND>(A, S, L, lane, Rq);
+        __builtin_amdgcn_sched_barrier(0);
+        grp_issue<UNG, NT>(A, I, L, lane, Rq, zero);
+        __builtin_amdgcn_sched_barrier(0);
+        grp_accum<UNG, KIND>(B, S, L, lane, Rq);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    wave_order();
+    return (uint16_t)L.res[lane];
+}
+
 // Dense-tile test (wave-uniform): every valid packet non-empty, starts and
 // ends non-decreasing, gaps below 4 KiB, and the range at most 9/8 of the
 // tile's bytes + 2 KiB.  Sets the range [A0, A0 + 16 T).
@@ -1070,15 +1248,15 @@ __device__ __forceinline__ bool seg_dense(int lane, uint64_t a, uint32_t len, bo
                                           uint32_t nvalid, uint64_t &A0, uint32_t &T)
 {
     const uint64_t e = a + len;
-    const uint64_t elast = __shfl(e, (int)nvalid - 1, 64);
+    const uint64_t elast = lane_u64(e, (int)nvalid - 1);
     const uint64_t s0 = valid ? a : elast, s1 = valid ? e : elast;
-    const uint64_t p0 = __shfl_up(s0, 1, 64), p1 = __shfl_up(s1, 1, 64);
+    const uint64_t p0 = wave_shr1_u64(s0), p1 = wave_shr1_u64(s1);
     const bool ok = !valid || (len != 0 && (lane == 0 ||
                                             (s0 >= p0 && s1 >= p1 && s0 < p1 + 4096u)));
     if (__ballot(!ok))
         return false;
-    const uint32_t sum = __shfl(wave_incl_sum(valid ? len : 0u), 63, 64);
-    A0 = __shfl(s0, 0, 64) & ~15ull;
+    const uint32_t sum = lane_u32(wave_incl_sum(valid ? len : 0u), 63);
+    A0 = lane_u64(s0, 0) & ~15ull;
     const uint64_t range = elast - A0;
     if (range > (uint64_t)sum + sum / 8u + 2048u)
         return false;
@@ -1089,15 +1267,16 @@ __device__ __forceinline__ bool seg_dense(int lane, uint64_t a, uint32_t len, bo
 // Ragged kernel with both paths: dense tiles stream their byte range
 // (seg_tile), the others take the flat path.  (The fused header checksum
 // stays on k_cksum_flat.)
-template <int UN, int UNS, int KIND, bool NT>
-__global__ void __launch_bounds__(256)
+template <int UN, int UNS, int UNG, int KIND, bool NT>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UNS >= 8 ? 2 : 4)))
 k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
             const uint16_t *__restrict__ lens, uint64_t n, uint16_t *__restrict__ out,
-            unsigned long long *__restrict__ bad, int variant)
+            unsigned long long *__restrict__ bad, int grp_thr, int variant)
 {
     (void)variant; // WC_VARIANT: A/B experiments
     union TileLds {
         FlatLds<UN> flat;
+        GrpLds grp;
         struct {
             u32x4 stage[64 * UNS]; // the row group's chunks
             uint32_t pre[64 * UNS];
@@ -1149,9 +1328,21 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
         uint32_t T = 0;
         uint16_t r;
         bool dense = seg_dense(lane, a, len, valid, nvalid, A0, T);
-        if constexpr (KIND == WC_KIND_PAYLOAD)
+        // Uniform tile?  Chunk fill of the grouped path's 1024 R slots.
+        const uint32_t nchg = valid ? ((uint32_t)(a & 15u) + len + 15u) >> 4 : 0u;
+        const uint32_t Rq = (wave_max(nchg) + 15u) >> 4;
+        const uint32_t fill = lane_u32(wave_incl_sum(nchg), 63);
+        const uint32_t thr = dense ? (uint32_t)(grp_thr & 0xFF) : (uint32_t)(grp_thr >> 8);
+        bool grouped = Rq != 0 && (uint64_t)fill * 64u >= (uint64_t)thr * 1024u * Rq;
+        if constexpr (KIND == WC_KIND_PAYLOAD) {
+            // payload_cksum needs the whole header inside the packet
+            const bool bad_hdr = __ballot(valid && len < max(ph.hl, 20u)) != 0;
+            grouped = grouped && !bad_hdr;
             dense = dense && !__ballot(valid && !seg_payload_ok(a, len, ph));
-        if (dense)
+        }
+        if (grouped)
+            r = grp_tile<UNG, KIND, NT>(L.grp, lane, a, len, valid, ph, Rq, zero, prefetch_hdr);
+        else if (dense)
             r = seg_tile<UNS, KIND, NT>(L.seg.pre, L.seg.stage, lane, a, len, ph, hdr.h1, A0, T,
                                         zero, prefetch_hdr);
         else
@@ -1281,19 +1472,26 @@ static hipError_t launch_flat_un(const LaunchArgs &a, hipStream_t st)
         return hipGetLastError();
     }
     if (a.seg_rows && !a.out_hdr) {
-#define WC_SEG(US)                                                             \
+#define WC_SEG(US, UG)                                                         \
     if (a.kind == WC_KIND_PAYLOAD)                                             \
-        hipLaunchKernelGGL((k_cksum_seg<UN, US, WC_KIND_PAYLOAD, true>), dim3(grid), \
-                           dim3(256), 0, st, b, a.offs, a.lens, a.n, a.out, bad, a.variant); \
+        hipLaunchKernelGGL((k_cksum_seg<UN, US, UG, WC_KIND_PAYLOAD, true>), dim3(grid), \
+                           dim3(256), 0, st, b, a.offs, a.lens, a.n, a.out, bad, a.grp_thr, \
+                           a.variant);                                         \
     else                                                                       \
-        hipLaunchKernelGGL((k_cksum_seg<UN, US, WC_KIND_IP, true>), dim3(grid), \
-                           dim3(256), 0, st, b, a.offs, a.lens, a.n, a.out, bad, a.variant);
+        hipLaunchKernelGGL((k_cksum_seg<UN, US, UG, WC_KIND_IP, true>), dim3(grid), \
+                           dim3(256), 0, st, b, a.offs, a.lens, a.n, a.out, bad, a.grp_thr, \
+                           a.variant);
+        // Row-group sizes: seg path a.seg_rows (WC_SEG_ROWS), grouped path
+        // a.grp_rows (WC_GRP_ROWS 4 or 2, with the default flat and seg
+        // sizes only; 6 and 8 measured no faster on netmap slots).
         if (a.seg_rows == 2) {
-            WC_SEG(2)
+            WC_SEG(2, 4)
         } else if (a.seg_rows == 8) {
-            WC_SEG(8)
+            WC_SEG(8, 4)
+        } else if (UN != 2 || a.grp_rows == 4) {
+            WC_SEG(4, 4)
         } else {
-            WC_SEG(4)
+            WC_SEG(4, 2)
         }
 #undef WC_SEG
         return hipGetLastError();
