@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--len", type=int, default=1472, help="packet bytes for c3")
     ap.add_argument("--kind", default="ip", choices=["ip", "payload"],
                     help="ip_cksum (default) or payload_cksum per packet")
+    ap.add_argument("--headers", action="store_true",
+                    help="stamp well-formed IPv4 / IPv6 UDP headers on every packet "
+                         "(synth.stamp_udp_headers) instead of random header bytes")
     ap.add_argument("--total-packets", type=int, default=1 << 28, help="c5 total")
     ap.add_argument("--window-packets", type=int, default=1 << 25, help="c5 resident window")
     ap.add_argument("--packets", type=int, default=1 << 20)
@@ -121,6 +124,9 @@ def make_workload(args, dev, rank, world):
         nbytes = n * L
         buf = torch.empty(nbytes + 64, dtype=torch.uint8, device=dev)
         wc.synth_fill(buf, seed, nbytes=nbytes)
+        if args.headers:
+            synth.stamp_udp_headers(buf, torch.arange(n, device=dev) * L,
+                                    torch.full((n,), L, device=dev))
         out = torch.empty(n, dtype=torch.uint16, device=dev)
 
         def step():
@@ -140,6 +146,8 @@ def make_workload(args, dev, rank, world):
     wc.synth_fill(buf, seed, nbytes=nbytes)
     d_off = torch.from_numpy(offs).to(dev)
     d_len = torch.from_numpy(lens).to(dev)
+    if args.headers:
+        synth.stamp_udp_headers(buf, d_off, d_len)
     out = torch.empty(n, dtype=torch.uint16, device=dev)
 
     def step():
@@ -299,7 +307,9 @@ def main():
             "scaling": scaling,
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic: splitmix64 payload bytes generated on device (wc_synth_fill)",
+            "data": "synthetic: splitmix64 payload bytes generated on device (wc_synth_fill)"
+                    + ("; well-formed IPv4 (IHL 5) / IPv6 UDP headers stamped 2:1"
+                       if args.headers else ""),
             "config": {"workload": desc, **meta, "parallelism": f"packet-shard x{world}",
                        "kernel_shape": plan, "payload_GBps": round(value * GIB / 1e9, 1)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1),

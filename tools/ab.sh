@@ -14,7 +14,8 @@ if [ -n "${VP:-}" ]; then
 fi
 T="timeout -k 10 200 python tools/tune.py --rounds ${ROUNDS:-6} --iters 20"
 for c in ${CASES:-c2:ip c2:payload}; do
-    cfg=${c%%:*}; kind=${c##*:}
+    cfg=${c%%:*}; kind=${c##*:}; hdr=""
+    case $kind in payload+h) kind=payload; hdr="--headers" ;; esac
     case $cfg in
         c2) a="--config c2" ;;
         c4) a="--config c4" ;;
@@ -24,6 +25,7 @@ for c in ${CASES:-c2:ip c2:payload}; do
         c3-*) a="--config c3 --len ${cfg#c3-}" ;;
     esac
     echo "== $c"
-    $T $a --kind $kind --variants "$VARS" > gpurun_out/ab_${cfg}_${kind}.log 2>&1 || { tail gpurun_out/ab_${cfg}_${kind}.log; exit 1; }
-    grep -v "^\s*round\|amdgpu.ids" gpurun_out/ab_${cfg}_${kind}.log
+    log=gpurun_out/ab_${cfg}_${kind}${hdr:+_h}.log
+    $T $a --kind $kind $hdr --variants "$VARS" > $log 2>&1 || { tail $log; exit 1; }
+    grep -v "^\s*round\|amdgpu.ids" $log
 done

@@ -67,6 +67,8 @@ def main():
     ap.add_argument("--kind", default="ip", choices=["ip", "payload"])
     ap.add_argument("--offset", type=int, default=0, help="byte offset of packet 0 (c2/c3)")
     ap.add_argument("--stride", type=int, default=0, help="packet stride (c2/c3; default len)")
+    ap.add_argument("--headers", action="store_true",
+                    help="well-formed IPv4 / IPv6 UDP headers (synth.stamp_udp_headers)")
     ap.add_argument("--ragged", action="store_true",
                     help="c2/c3 through the ragged entry point (offset/length arrays)")
     args = ap.parse_args()
@@ -82,6 +84,8 @@ def main():
         buf = torch.empty(nbytes + 64, dtype=torch.uint8, device=dev)
         wc.synth_fill(buf, 1, nbytes=nbytes)
         d_off, d_len = torch.from_numpy(offs).to(dev), torch.from_numpy(lens).to(dev)
+        if args.headers:
+            synth.stamp_udp_headers(buf, d_off, d_len)
         out = torch.empty(n, dtype=torch.uint16, device=dev)
         run = lambda: wc.cksum_ragged(buf, d_off, d_len, out=out, kind=args.kind)  # noqa: E731
     else:
@@ -91,6 +95,9 @@ def main():
         nbytes = n * L
         buf = torch.empty(args.offset + n * stride + 64, dtype=torch.uint8, device=dev)
         wc.synth_fill(buf, 1)
+        if args.headers:
+            synth.stamp_udp_headers(buf, torch.arange(n, device=dev) * stride + args.offset,
+                                    torch.full((n,), L, device=dev))
         out = torch.empty(n, dtype=torch.uint16, device=dev)
         run = lambda: wc.cksum_strided(buf, stride, L, n, out=out, kind=args.kind,  # noqa: E731
                                        byte_offset=args.offset)

@@ -32,3 +32,36 @@ def packed_offsets(lengths: np.ndarray, lead: int = 0) -> np.ndarray:
     if lead:
         off[1:] += np.uint64(lead)
     return off
+
+
+def stamp_udp_headers(buf, offs, lens, v6_every: int = 3, chunk: int = 1 << 21) -> None:
+    """Turn packet i of a synthetic batch into a well-formed UDP datagram in
+    place, on the device: IPv6 (every `v6_every`-th packet) or IPv4 with IHL 5
+    (ip4.h:55-66, ip6.h:45-57, udp.h:41-46), next header / protocol 17, IP
+    and UDP lengths matching `lens`, UDP checksum 0.  The other header bytes
+    (ports, addresses, TTL, ...) stay random.  This is what a netmap TX queue
+    or RX ring holds, as opposed to random bytes read as IP headers (random
+    version, IHL and next_hdr).  `buf`: uint8 device tensor; `offs` / `lens`:
+    packet offsets and lengths (numpy or tensors); every len >= 48."""
+    import torch
+
+    dev = buf.device
+    n = int(offs.shape[0])
+    o_all = torch.as_tensor(np.asarray(offs, dtype=np.int64) if isinstance(offs, np.ndarray)
+                            else offs.to(torch.int64), device=dev)
+    l_all = torch.as_tensor(np.asarray(lens, dtype=np.int64) if isinstance(lens, np.ndarray)
+                            else lens.to(torch.int64) & 0xFFFF, device=dev)
+    for s in range(0, n, chunk):
+        o = o_all[s:s + chunk]
+        ln = l_all[s:s + chunk]
+        v6 = (torch.arange(s, s + o.numel(), device=dev) % v6_every) == 0
+        for sel, fields in (
+            (~v6, lambda L: [(0, 0x45), (2, L >> 8), (3, L), (9, 17),
+                             (24, (L - 20) >> 8), (25, L - 20), (26, 0), (27, 0)]),
+            (v6, lambda L: [(0, 0x60), (4, (L - 40) >> 8), (5, L - 40), (6, 17),
+                            (44, (L - 40) >> 8), (45, L - 40), (46, 0), (47, 0)]),
+        ):
+            oo, LL = o[sel], ln[sel]
+            for at, val in fields(LL):
+                v = val if torch.is_tensor(val) else torch.full_like(oo, val)
+                buf[oo + at] = (v & 0xFF).to(torch.uint8)
