@@ -8,7 +8,8 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp WC_NO_BUILD=1
 T="timeout -k 10 120 python tools/tune.py --rounds ${ROUNDS:-4} --iters 20"
 for c in ${CASES:-c4:payload}; do
-    cfg=${c%%:*}; kind=${c##*:}
+    cfg=${c%%:*}; kind=${c##*:}; hdr=""
+    case $kind in payload+h) kind=payload; hdr="--headers" ;; esac
     case $cfg in
         c2) a="--config c2" ;;
         c4) a="--config c4" ;;
@@ -19,7 +20,7 @@ for c in ${CASES:-c4:payload}; do
     esac
     echo "== $c"
     for rep in 1 2; do
-        echo -n "prev "; WC_LIB=tools/libwccksum_prev.so $T $a --kind $kind 2>&1 | grep -v amdgpu.ids || exit 1
-        echo -n "new  "; $T $a --kind $kind 2>&1 | grep -v amdgpu.ids || exit 1
+        echo -n "prev "; WC_LIB=tools/libwccksum_prev.so $T $a --kind $kind $hdr 2>&1 | grep -v amdgpu.ids || exit 1
+        echo -n "new  "; $T $a --kind $kind $hdr 2>&1 | grep -v amdgpu.ids || exit 1
     done
 done

@@ -662,21 +662,47 @@ __device__ __forceinline__ void flat_accum(const FlatRows<UN> &R, FlatLds<UN> &L
     wave_order(); // pre is rewritten by the next group
 }
 
-// Header bytes 0, 2, 3, 6 of a packet (payload_cksum), packed b0 | b2 << 8 |
-// b3 << 16 | b6 << 24.  ONE 16-byte load from the 8-byte boundary at or below
-// the packet start (a scattered load moves a whole cache line per lane, so
-// one load instead of four byte loads): [a & ~7, +16) lies in a's own 8-byte
-// block or within the 20 header bytes payload_cksum reads anyway
-// (in_cksum.c:149-151), so it never touches a page the reference would not.
+// payload_cksum's header bytes, prefetched a tile ahead: ONE 16-byte load at
+// the 4-byte boundary at or below the packet start (a scattered load moves a
+// whole cache line per lane, so one load instead of several byte loads).  It
+// covers packet bytes 0..12, inside the header the reference reads anyway
+// (in_cksum.c:142-160), so it never touches a page the reference would not.
+// The bytes are picked out at their use (hdr_h0 / hdr_h1), not at the load:
+// extracting them right away made hipcc wait for the load -- and for every
+// stream load issued before it -- at the prefetch.
 typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
-__device__ __forceinline__ uint32_t load_hdr4(uint64_t a)
+
+struct HdrRaw {
+    u32x4 d;
+};
+
+__device__ __forceinline__ HdrRaw load_hdr(uint64_t a)
 {
-    const u32x4a4 d = *(const u32x4a4 __attribute__((address_space(1))) *)(uintptr_t)(a & ~7ull);
-    const uint32_t sh = 8u * (uint32_t)(a & 7u);
-    const uint64_t lo = (uint64_t)d.x | ((uint64_t)d.y << 32);
-    const uint64_t hi = (uint64_t)d.z | ((uint64_t)d.w << 32);
-    const uint64_t w = sh ? (lo >> sh) | (hi << (64u - sh)) : lo; // packet bytes 0..7
-    return __builtin_amdgcn_perm((uint32_t)(w >> 32), (uint32_t)w, 0x06030200u);
+    return HdrRaw{*(const u32x4a4 __attribute__((address_space(1))) *)(uintptr_t)(a & ~3ull)};
+}
+
+// b0 | b2 << 8 | b3 << 16 | b6 << 24 of the packet at a.
+__device__ __forceinline__ uint32_t hdr_h0(const HdrRaw &h, uint64_t a)
+{
+    const uint32_t sh = 8u * (uint32_t)(a & 3u);
+    const uint32_t w0 = __builtin_amdgcn_alignbit(h.d.y, h.d.x, sh); // bytes 0..3
+    const uint32_t w1 = __builtin_amdgcn_alignbit(h.d.z, h.d.y, sh); // bytes 4..7
+    return __builtin_amdgcn_perm(w1, w0, 0x06030200u);
+}
+
+// b4 | b5 << 8 | b9 << 16 of the packet at a.
+__device__ __forceinline__ uint32_t hdr_h1(const HdrRaw &h, uint64_t a)
+{
+    const uint32_t sh = 8u * (uint32_t)(a & 3u);
+    const uint32_t w1 = __builtin_amdgcn_alignbit(h.d.z, h.d.y, sh); // bytes 4..7
+    const uint32_t w2 = __builtin_amdgcn_alignbit(h.d.w, h.d.z, sh); // bytes 8..11
+    return __builtin_amdgcn_perm(w2, w1, 0x0C050100u);
+}
+
+__device__ __forceinline__ PseudoHdr hdr_pseudo(const HdrRaw &h, uint64_t a)
+{
+    const uint32_t h0 = hdr_h0(h, a);
+    return pseudo_hdr(h0 & 0xFFu, (h0 >> 8) & 0xFFu, (h0 >> 16) & 0xFFu, h0 >> 24);
 }
 
 // Fused IPv4 header checksum for the flat kernel: the packet's own lane sums
@@ -757,6 +783,19 @@ __device__ __forceinline__ uint32_t flat_tile_sum(FlatLds<UN> &L, const WeightLu
     return acc;
 }
 
+// Packet p's offset and length, or packet 0's offset and length 0 past the
+// batch end -- with unconditional loads.
+__device__ __forceinline__ void meta_load(const uint64_t *__restrict__ offs,
+                                          const uint16_t *__restrict__ lens, uint64_t p,
+                                          uint64_t n, uint64_t &off, uint32_t &len)
+{
+    const bool v = p < n;
+    const uint64_t pc = v ? p : 0;
+    off = offs[pc];
+    const uint32_t l = lens[pc];
+    len = v ? l : 0u;
+}
+
 template <int UN, int KIND, bool NT, bool HDR, bool NOLOAD = false>
 __global__ void __launch_bounds__(256)
 k_cksum_flat(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
@@ -778,37 +817,38 @@ k_cksum_flat(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
     uint64_t tile = (uint64_t)blockIdx.x * kFlatWaves + w;
     uint32_t nbad = 0;
 
-    // Metadata (and payload header bytes) of the first tile.
+    // Metadata (and payload header bytes) of the first tile.  All prefetch
+    // loads are unconditional (lanes past the batch end re-read packet 0):
+    // a load under a branch leaves hipcc's wait counting no choice but
+    // vmcnt(0), which would wait for the prefetch itself.
     uint64_t p = tile * 64 + lane;
-    uint64_t off_n = p < n ? offs[p] : 0;
-    uint32_t len_n = p < n ? (uint32_t)lens[p] : 0u;
-    uint32_t hdr_n = 0;
+    uint64_t off_n;
+    uint32_t len_n;
+    meta_load(offs, lens, p, n, off_n, len_n);
+    HdrRaw hdr_n{};
     if constexpr (KIND == WC_KIND_PAYLOAD)
-        hdr_n = p < n ? load_hdr4((uint64_t)base + off_n) : 0u;
+        hdr_n = load_hdr((uint64_t)base + off_n);
 
     for (; tile < ntiles; tile += nwaves) {
         p = tile * 64 + lane;
         const bool valid = p < n;
         const uint64_t off = off_n;
         const uint32_t len = len_n;
-        const uint32_t hdr4 = hdr_n;
+        const HdrRaw hdr = hdr_n;
         const uint64_t pn = (tile + nwaves) * 64 + lane;
-        const bool valid_n = pn < n;
-        off_n = valid_n ? offs[pn] : 0; // prefetch the next tile's metadata
-        len_n = valid_n ? (uint32_t)lens[pn] : 0u;
+        meta_load(offs, lens, pn, n, off_n, len_n); // prefetch the next tile's metadata
 
         const uint64_t a = (uint64_t)base + off;
         PseudoHdr ph{0u, 1u, 0u};
         if constexpr (KIND == WC_KIND_PAYLOAD)
             if (valid)
-                ph = pseudo_hdr(hdr4 & 0xFFu, (hdr4 >> 8) & 0xFFu, (hdr4 >> 16) & 0xFFu,
-                                hdr4 >> 24);
+                ph = hdr_pseudo(hdr, a);
         // The next tile's header bytes: issued once its offsets are back,
         // behind this tile's first loads.
         const uint32_t acc = flat_tile_sum<UN, KIND, NT, NOLOAD, false>(
             L, &lut, lane, a, len, valid, ph, [&] {
                 if constexpr (KIND == WC_KIND_PAYLOAD)
-                    hdr_n = valid_n ? load_hdr4((uint64_t)base + off_n) : 0u;
+                    hdr_n = load_hdr((uint64_t)base + off_n);
             });
 
         const uint16_t r = fold_not(acc);
@@ -859,7 +899,7 @@ k_cksum_flat(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
 // with IHL 5, IPv6 @8..39), so body + src/dst is ONE range of the running sum,
 // [a + 12, a + len) or [a + 8, a + len).  The lone field bytes (IPv4 proto @9,
 // IPv6 payload length @4..5) come from the header load that is prefetched a
-// tile ahead anyway (load_hdr7), and an IPv4 header with options (or a
+// tile ahead anyway (load_hdr), and an IPv4 header with options (or a
 // malformed IHL < 5) corrects the range by the bytes between byte 20 and hl,
 // from a few masked loads of those lanes alone.  Then the non-linear term
 // `special` (IPv4 plen, IPv6 next_hdr << 24) is added.  The reference adds it
@@ -908,26 +948,6 @@ __device__ __forceinline__ uint32_t seg_range(const u32x4 &d, int co, int lo, in
     for (int j = 0; j < 4; ++j)
         v = wsum(pick_dword(d, j) & (expand_nibble(kb, j) * 0xFFu), v);
     return v;
-}
-
-// Header bytes a payload_cksum lane needs before its tile, from ONE 16-byte
-// load at the 4-byte boundary at or below the packet start (covers packet
-// bytes 0..12, all inside the header the reference reads, in_cksum.c:142-160):
-// h0 = b0 | b2 << 8 | b3 << 16 | b6 << 24 (as load_hdr4), h1 = b4 | b5 << 8 |
-// b9 << 16.
-struct Hdr7 {
-    uint32_t h0, h1;
-};
-
-__device__ __forceinline__ Hdr7 load_hdr7(uint64_t a)
-{
-    const u32x4a4 d = *(const u32x4a4 __attribute__((address_space(1))) *)(uintptr_t)(a & ~3ull);
-    const uint32_t sh = 8u * (uint32_t)(a & 3u);
-    const uint32_t w0 = __builtin_amdgcn_alignbit(d.y, d.x, sh); // bytes 0..3
-    const uint32_t w1 = __builtin_amdgcn_alignbit(d.z, d.y, sh); // bytes 4..7
-    const uint32_t w2 = __builtin_amdgcn_alignbit(d.w, d.z, sh); // bytes 8..11
-    return Hdr7{__builtin_amdgcn_perm(w1, w0, 0x06030200u),
-                __builtin_amdgcn_perm(w2, w1, 0x0C050100u)};
 }
 
 template <int UNS>
@@ -1019,12 +1039,29 @@ __device__ __forceinline__ bool seg_payload_ok(uint64_t a, uint32_t len, const P
 // Returns the checksum.
 template <int UNS, int KIND, bool NT, class F>
 __device__ __forceinline__ uint16_t seg_tile(uint32_t *pre, u32x4 *stage, int lane, uint64_t a,
-                                             uint32_t len, const PseudoHdr &ph, uint32_t h1,
+                                             uint32_t len, bool valid, const HdrRaw &hdr,
                                              uint64_t A0, uint32_t T, uint64_t zero,
-                                             F &&after_first_issue)
+                                             F &&after_first_issue, bool &done)
 {
     constexpr uint32_t kGrp = 64u * UNS;
     constexpr bool PL = KIND == WC_KIND_PAYLOAD;
+    // The stream's first row group goes out before the header bytes are
+    // waited for: its range depends on the offsets and lengths alone.
+    SegRows<UNS> A, B;
+    seg_issue<UNS, NT>(A, A0, 0, lane, T, zero);
+    after_first_issue();
+    __builtin_amdgcn_sched_barrier(0); // keep the header wait behind the issue
+
+    PseudoHdr ph{0u, 1u, 0u};
+    if constexpr (PL) {
+        if (valid)
+            ph = hdr_pseudo(hdr, a);
+        if (__ballot(valid && !seg_payload_ok(a, len, ph))) {
+            done = false; // the caller takes the exact flat path
+            return 0;
+        }
+    }
+    done = true;
     const uint32_t f1 = PL ? (ph.v4 ? 12u : 8u) : 0u;
     const uint64_t rs = a + f1 - A0, re = a + len - A0;
     const uint32_t cs = (uint32_t)(rs >> 4), qs = (uint32_t)(rs & 15u);
@@ -1032,7 +1069,7 @@ __device__ __forceinline__ uint16_t seg_tile(uint32_t *pre, u32x4 *stage, int la
 
     // payload_cksum, IPv4 with hl != 20: V of the bytes between 20 and hl
     // (<= 40 bytes, <= 4 chunks), loaded by those lanes alone and summed
-    // before the stream starts, so the chunks hold no registers across it.
+    // before the stream goes on, so the chunks hold no registers across it.
     const bool corr = PL && ph.v4 && ph.hl != 20u;
     uint32_t cv = 0;
     if constexpr (PL) {
@@ -1049,10 +1086,6 @@ __device__ __forceinline__ uint16_t seg_tile(uint32_t *pre, u32x4 *stage, int la
                 cv += seg_range(xc[k], (int)(ca - a) + 16 * k, clo, chi);
         }
     }
-
-    SegRows<UNS> A, B;
-    seg_issue<UNS, NT>(A, A0, 0, lane, T, zero);
-    after_first_issue();
 
     uint32_t carry = 0, Ps = 0, Pe = 0;
     u32x4 hs = {0u, 0u, 0u, 0u}, he = {0u, 0u, 0u, 0u};
@@ -1075,6 +1108,7 @@ __device__ __forceinline__ uint16_t seg_tile(uint32_t *pre, u32x4 *stage, int la
         // Lone field bytes at their address weight: IPv4 proto @9 (odd
         // offset), IPv6 payload length @4..5 (a word at an even offset).
         const uint32_t odd = (uint32_t)(a & 1u);
+        const uint32_t h1 = hdr_h1(hdr, a);
         const uint32_t b9 = (h1 >> 16) & 0xFFu, b4 = h1 & 0xFFu, b5 = (h1 >> 8) & 0xFFu;
         v += ph.v4 ? (odd ? b9 : b9 << 8) : (odd ? (b4 << 8) | b5 : b4 | (b5 << 8));
         // hl < 20: the body starts early (src/dst count twice, as in the
@@ -1135,16 +1169,25 @@ struct GrpRows {
     u32x4 d[UNG];
 };
 
+// Bytes a packet's chunks cover: payload_cksum reads the IPv4 header fields
+// up to byte 19 whatever len is (in_cksum.c:149-151).
+template <int KIND>
+__device__ __forceinline__ uint32_t grp_span(uint32_t len)
+{
+    return KIND == WC_KIND_PAYLOAD && len ? max(len, 20u) : len;
+}
+
+template <int KIND>
 __device__ __forceinline__ void grp_load_quad(GrpIssue &I, const GrpLds &L, int lane)
 {
     const GrpDesc g = L.gd[min(4u * I.q + ((uint32_t)lane >> 4), 63u)];
     const uint64_t a = (uint64_t)g.a_lo | ((uint64_t)g.a_hi << 32);
-    const uint32_t len = g.info & 0xFFFFu;
+    const uint32_t span = grp_span<KIND>(g.info & 0xFFFFu);
     I.cb = a & ~15ull;
-    I.nch = I.q < 16u && len ? (uint32_t)((a & 15u) + len + 15u) >> 4 : 0u;
+    I.nch = I.q < 16u && span ? (uint32_t)((a & 15u) + span + 15u) >> 4 : 0u;
 }
 
-template <int UNG, bool NT>
+template <int UNG, int KIND, bool NT>
 __device__ __forceinline__ void grp_issue(GrpRows<UNG> &R, GrpIssue &I, const GrpLds &L,
                                           int lane, uint32_t Rq, uint64_t zero)
 {
@@ -1155,7 +1198,7 @@ __device__ __forceinline__ void grp_issue(GrpRows<UNG> &R, GrpIssue &I, const Gr
         if (++I.k == Rq) { // wave-uniform
             I.k = 0;
             ++I.q;
-            grp_load_quad(I, L, lane);
+            grp_load_quad<KIND>(I, L, lane);
         }
     }
 }
@@ -1186,7 +1229,8 @@ __device__ __forceinline__ void grp_accum(const GrpRows<UNG> &R, GrpAcc &S, GrpL
     for (int u = 0; u < UNG; ++u) {
         if (S.q < 16u) { // wave-uniform: rows past the tile's last quad are idle
             const uint32_t c = 16u * S.k + gl;
-            const uint32_t nch = S.len ? (S.s + S.len + 15u) >> 4 : 0u;
+            const uint32_t span = grp_span<KIND>(S.len);
+            const uint32_t nch = span ? (S.s + span + 15u) >> 4 : 0u;
             uint32_t eh = 0, oh = 0;
             accum_strided<KIND, false, false>(R.d[u], 16 * (int)c - (int)S.s,
                                               KIND == WC_KIND_PAYLOAD ? (int)S.hl : 0,
@@ -1210,29 +1254,46 @@ __device__ __forceinline__ void grp_accum(const GrpRows<UNG> &R, GrpAcc &S, GrpL
     }
 }
 
-// One uniform tile.  Returns this lane's packet's checksum.
+// One uniform tile.  Returns this lane's packet's checksum, or done = false
+// (payload_cksum with a header longer than its packet: the caller takes the
+// flat path).
 template <int UNG, int KIND, bool NT, class F>
 __device__ __forceinline__ uint16_t grp_tile(GrpLds &L, int lane, uint64_t a, uint32_t len,
-                                             bool valid, const PseudoHdr &ph, uint32_t Rq,
-                                             uint64_t zero, F &&after_first_issue)
+                                             bool valid, const HdrRaw &hdr, uint32_t Rq,
+                                             uint64_t zero, F &&after_first_issue, bool &done)
 {
-    L.gd[lane] = GrpDesc{(uint32_t)a, (uint32_t)(a >> 32),
-                         (valid ? len : 0u) | (ph.hl << 16) | (ph.v4 << 24), ph.special};
+    // Addresses first: the first row group goes out before the header bytes
+    // are waited for.
+    L.gd[lane] = GrpDesc{(uint32_t)a, (uint32_t)(a >> 32), valid ? len : 0u, 0u};
     wave_order();
     GrpIssue I{0u, 0u, 0ull, 0u};
-    grp_load_quad(I, L, lane);
+    grp_load_quad<KIND>(I, L, lane);
+    GrpRows<UNG> A, B;
+    grp_issue<UNG, KIND, NT>(A, I, L, lane, Rq, zero);
+    after_first_issue();
+    __builtin_amdgcn_sched_barrier(0); // keep the header wait behind the issue
+    if constexpr (KIND == WC_KIND_PAYLOAD) {
+        PseudoHdr ph{0u, 1u, 0u};
+        if (valid)
+            ph = hdr_pseudo(hdr, a);
+        if (__ballot(valid && len < max(ph.hl, 20u))) {
+            done = false;
+            return 0;
+        }
+        L.gd[lane].info |= (ph.hl << 16) | (ph.v4 << 24);
+        L.gd[lane].special = ph.special;
+        wave_order();
+    }
+    done = true;
     GrpAcc S{};
     grp_acc_quad(S, L, lane);
     const uint32_t rows = 16u * Rq;
-    GrpRows<UNG> A, B;
-    grp_issue<UNG, NT>(A, I, L, lane, Rq, zero);
-    after_first_issue();
     for (uint32_t j = 0; j < rows; j += 2u * UNG) {
-        grp_issue<UNG, NT>(B, I, L, lane, Rq, zero);
+        grp_issue<UNG, KIND, NT>(B, I, L, lane, Rq, zero);
         __builtin_amdgcn_sched_barrier(0);
         grp_accum<UNG, KIND>(A, S, L, lane, Rq);
         __builtin_amdgcn_sched_barrier(0);
-        grp_issue<UNG, NT>(A, I, L, lane, Rq, zero);
+        grp_issue<UNG, KIND, NT>(A, I, L, lane, Rq, zero);
         __builtin_amdgcn_sched_barrier(0);
         grp_accum<UNG, KIND>(B, S, L, lane, Rq);
         __builtin_amdgcn_sched_barrier(0);
@@ -1293,13 +1354,14 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     uint32_t nbad = 0;
     const uint64_t zero = (uint64_t)(uintptr_t)&kZeroChunk;
 
+    // Unconditional prefetch loads, as in k_cksum_flat.
     uint64_t p = tile * 64 + lane;
-    uint64_t off_n = p < n ? offs[p] : 0;
-    uint32_t len_n = p < n ? (uint32_t)lens[p] : 0u;
-    Hdr7 hdr_n{0u, 0u};
+    uint64_t off_n;
+    uint32_t len_n;
+    meta_load(offs, lens, p, n, off_n, len_n);
+    HdrRaw hdr_n{};
     if constexpr (KIND == WC_KIND_PAYLOAD)
-        if (p < n)
-            hdr_n = load_hdr7((uint64_t)base + off_n);
+        hdr_n = load_hdr((uint64_t)base + off_n);
 
     for (; tile < ntiles; tile += nwaves) {
         p = tile * 64 + lane;
@@ -1307,47 +1369,45 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
         const uint32_t nvalid = (uint32_t)min<uint64_t>(64, n - tile * 64);
         const uint64_t off = off_n;
         const uint32_t len = len_n;
-        const Hdr7 hdr = hdr_n;
+        const HdrRaw hdr = hdr_n;
         const uint64_t pn = (tile + nwaves) * 64 + lane;
-        const bool valid_n = pn < n;
-        off_n = valid_n ? offs[pn] : 0;
-        len_n = valid_n ? (uint32_t)lens[pn] : 0u;
+        meta_load(offs, lens, pn, n, off_n, len_n);
+        bool prefetched = false;
         auto prefetch_hdr = [&] {
             if constexpr (KIND == WC_KIND_PAYLOAD)
-                if (valid_n)
-                    hdr_n = load_hdr7((uint64_t)base + off_n);
+                if (!prefetched) // wave-uniform
+                    hdr_n = load_hdr((uint64_t)base + off_n);
+            prefetched = true;
         };
 
         const uint64_t a = (uint64_t)base + off;
-        PseudoHdr ph{0u, 1u, 0u};
-        if constexpr (KIND == WC_KIND_PAYLOAD)
-            if (valid)
-                ph = pseudo_hdr(hdr.h0 & 0xFFu, (hdr.h0 >> 8) & 0xFFu, (hdr.h0 >> 16) & 0xFFu,
-                                hdr.h0 >> 24);
         uint64_t A0 = 0;
         uint32_t T = 0;
-        uint16_t r;
-        bool dense = seg_dense(lane, a, len, valid, nvalid, A0, T);
+        uint16_t r = 0;
+        const bool dense = seg_dense(lane, a, len, valid, nvalid, A0, T);
         // Uniform tile?  Chunk fill of the grouped path's 1024 R slots.
-        const uint32_t nchg = valid ? ((uint32_t)(a & 15u) + len + 15u) >> 4 : 0u;
+        const uint32_t span = grp_span<KIND>(len);
+        const uint32_t nchg = valid ? ((uint32_t)(a & 15u) + span + 15u) >> 4 : 0u;
         const uint32_t Rq = (wave_max(nchg) + 15u) >> 4;
         const uint32_t fill = lane_u32(wave_incl_sum(nchg), 63);
         const uint32_t thr = dense ? (uint32_t)(grp_thr & 0xFF) : (uint32_t)(grp_thr >> 8);
-        bool grouped = Rq != 0 && (uint64_t)fill * 64u >= (uint64_t)thr * 1024u * Rq;
-        if constexpr (KIND == WC_KIND_PAYLOAD) {
-            // payload_cksum needs the whole header inside the packet
-            const bool bad_hdr = __ballot(valid && len < max(ph.hl, 20u)) != 0;
-            grouped = grouped && !bad_hdr;
-            dense = dense && !__ballot(valid && !seg_payload_ok(a, len, ph));
-        }
+        const bool grouped = Rq != 0 && (uint64_t)fill * 64u >= (uint64_t)thr * 1024u * Rq;
+        bool done = false;
         if (grouped)
-            r = grp_tile<UNG, KIND, NT>(L.grp, lane, a, len, valid, ph, Rq, zero, prefetch_hdr);
+            r = grp_tile<UNG, KIND, NT>(L.grp, lane, a, len, valid, hdr, Rq, zero, prefetch_hdr,
+                                        done);
         else if (dense)
-            r = seg_tile<UNS, KIND, NT>(L.seg.pre, L.seg.stage, lane, a, len, ph, hdr.h1, A0, T,
-                                        zero, prefetch_hdr);
-        else
+            r = seg_tile<UNS, KIND, NT>(L.seg.pre, L.seg.stage, lane, a, len, valid, hdr, A0, T,
+                                        zero, prefetch_hdr, done);
+        if (!done) {
+            PseudoHdr ph{0u, 1u, 0u};
+            if constexpr (KIND == WC_KIND_PAYLOAD)
+                if (valid)
+                    ph = hdr_pseudo(hdr, a);
+            wave_order();
             r = fold_not(flat_tile_sum<UN, KIND, NT, false, true>(L.flat, nullptr, lane, a, len,
                                                                   valid, ph, prefetch_hdr));
+        }
         if (valid && out)
             out[p] = r;
         nbad += valid && r != 0;
