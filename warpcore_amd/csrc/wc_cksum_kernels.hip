@@ -894,22 +894,25 @@ k_cksum_flat(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
 // fold (in_cksum.c:74-80) maps positive numbers to [1, 0xFFFF] by their
 // residue, so fold(rotl32(V, 8)) is bit-exact.
 //
-// payload_cksum (in_cksum.c:140-167) needs no header pass either.  Its
-// pseudo-header src/dst fields end where a standard header ends (IPv4 @12..19
-// with IHL 5, IPv6 @8..39), so body + src/dst is ONE range of the running sum,
-// [a + 12, a + len) or [a + 8, a + len).  The lone field bytes (IPv4 proto @9,
-// IPv6 payload length @4..5) come from the header load that is prefetched a
-// tile ahead anyway (load_hdr), and an IPv4 header with options (or a
-// malformed IHL < 5) corrects the range by the bytes between byte 20 and hl,
-// from a few masked loads of those lanes alone.  Then the non-linear term
-// `special` (IPv4 plen, IPv6 next_hdr << 24) is added.  The reference adds it
-// in a uint32 that may wrap (next_hdr << 24, in_cksum.c:157).  For an even
-// start V is the exact accumulator, so V + special wraps exactly as the
-// reference does.  For an odd start the residue is exact as long as the
-// reference's sum does not wrap; a tile holding an odd-start packet that
-// could wrap (IPv6, next_hdr >= ~254 at 1500 B) takes the exact flat path
-// instead (seg_wrap_risk), as does one holding a packet shorter than its
-// header.
+// payload_cksum (in_cksum.c:140-167) needs no header pass and no header load
+// either.  Its pseudo-header src/dst fields end where a standard header ends
+// (IPv4 @12..19 with IHL 5, IPv6 @8..39), so body + src/dst is essentially ONE
+// range of the running sum, taken as [a + 8, a + len) for both versions.  The
+// header bytes 0..11 come out of the stream itself (the lane picks up its
+// packet's first two staged chunks, seg_accum): IPv6 adds its payload length
+// word @4, IPv4 takes out bytes 8..11 and adds proto << 8 (@9), and an IPv4
+// header with options (or a malformed IHL < 5) corrects the range by the
+// bytes between byte 20 and hl, from a few masked loads of those lanes alone.
+// Then the non-linear term `special` (IPv4 plen, IPv6 next_hdr << 24) is
+// added.  The reference adds it in a uint32 that may wrap (next_hdr << 24,
+// in_cksum.c:157).  For an even start V is the exact accumulator, so
+// V + special wraps exactly as the reference does.  For an odd start the
+// residue is exact as long as the reference's sum does not wrap; a tile
+// holding an odd-start packet that could wrap (IPv6, next_hdr >= ~254 at
+// 1500 B) is redone on the exact flat path (seg_wrap_risk), as is one holding
+// a packet shorter than its header.  A separate scattered header load per
+// packet cost 14 % of the C4 time (one more cache line per lane, not latency:
+// profiles/ab_r01_c4_payload_hdr.log).
 
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
@@ -969,12 +972,14 @@ __device__ __forceinline__ void seg_issue(SegRows<UNS> &R, uint64_t A0, uint32_t
 // Sum the UNS rows of the group at slot g0: row prefix sums (DPP), chained
 // through LDS; packet lanes whose start / end chunk falls in the group pick
 // up the running sum before it and the chunk itself.  `carry` is the running
-// sum before the group (wave-uniform).
-template <int UNS>
+// sum before the group (wave-uniform).  With HC (payload_cksum) the lane also
+// picks up its packet's first two chunks c0, c0 + 1 -- its header bytes
+// 0..11, and the start chunk cs, which is one of them.
+template <int UNS, bool HC>
 __device__ __forceinline__ void seg_accum(const SegRows<UNS> &R, uint32_t *pre, u32x4 *stage,
                                           uint32_t g0, int lane, uint32_t cs, uint32_t ce,
-                                          uint32_t &carry, uint32_t &Ps, uint32_t &Pe,
-                                          u32x4 &hs, u32x4 &he)
+                                          uint32_t c0, uint32_t &carry, uint32_t &Ps,
+                                          uint32_t &Pe, u32x4 &hs, u32x4 &he, u32x4 &h1)
 {
     constexpr uint32_t kGrp = 64u * UNS;
     uint32_t P[UNS];
@@ -1002,8 +1007,16 @@ __device__ __forceinline__ void seg_accum(const SegRows<UNS> &R, uint32_t *pre, 
     const uint32_t ds = cs - g0, de = ce - g0;
     // The packet's first / last chunk, for its partial sums (exec-masked
     // LDS reads: no scattered global re-loads).
-    if (ds < kGrp)
-        hs = stage[ds];
+    if constexpr (HC) {
+        const uint32_t d0 = c0 - g0; // (unsigned: c0 + 1 == g0 gives d0 + 1 == 0)
+        if (d0 < kGrp)
+            hs = stage[d0];
+        if (d0 + 1u < kGrp)
+            h1 = stage[d0 + 1u];
+    } else {
+        if (ds < kGrp)
+            hs = stage[ds];
+    }
     if (de < kGrp)
         he = stage[de];
     const uint32_t vs = pre[min(ds - 1u, kGrp - 1u)];
@@ -1014,6 +1027,23 @@ __device__ __forceinline__ void seg_accum(const SegRows<UNS> &R, uint32_t *pre, 
         Pe = de ? ve : carry;
     carry = c;
     wave_order(); // pre is rewritten by the next group
+}
+
+// Dword k (0..7) of the 32-byte window x:y.
+__device__ __forceinline__ uint32_t win_dword(const u32x4 &x, const u32x4 &y, uint32_t k)
+{
+    const u32x4 &h = k & 4u ? y : x;
+    return pick_dword(h, (int)(k & 3u));
+}
+
+// Packet bytes 4 m .. 4 m + 3 from the window x:y that holds the packet's
+// first bytes from offset s on.
+__device__ __forceinline__ uint32_t win_bytes(const u32x4 &x, const u32x4 &y, uint32_t s,
+                                              uint32_t m)
+{
+    const uint32_t k = (s >> 2) + m;
+    return __builtin_amdgcn_alignbit(win_dword(x, y, k + 1u), win_dword(x, y, k),
+                                     8u * (s & 3u));
 }
 
 // Could the reference's uint32 sum for this odd-start payload packet wrap
@@ -1035,96 +1065,99 @@ __device__ __forceinline__ bool seg_payload_ok(uint64_t a, uint32_t len, const P
 }
 
 // One dense tile.  [a, a + len) is this lane's packet; ip_cksum sums all of
-// it, payload_cksum the range [a + f1, a + len) plus the corrections above.
-// Returns the checksum.
-template <int UNS, int KIND, bool NT, class F>
+// it, payload_cksum the range [a + 8, a + len) corrected as below.  Returns
+// the checksum, or done = false when a payload_cksum lane can't be summed
+// here (header longer than the packet, possible uint32 wrap): the caller
+// then takes the exact flat path for the tile.
+template <int UNS, int KIND, bool NT>
 __device__ __forceinline__ uint16_t seg_tile(uint32_t *pre, u32x4 *stage, int lane, uint64_t a,
-                                             uint32_t len, bool valid, const HdrRaw &hdr,
-                                             uint64_t A0, uint32_t T, uint64_t zero,
-                                             F &&after_first_issue, bool &done)
+                                             uint32_t len, bool valid, uint64_t A0, uint32_t T,
+                                             uint64_t zero, bool &done)
 {
     constexpr uint32_t kGrp = 64u * UNS;
     constexpr bool PL = KIND == WC_KIND_PAYLOAD;
-    // The stream's first row group goes out before the header bytes are
-    // waited for: its range depends on the offsets and lengths alone.
-    SegRows<UNS> A, B;
-    seg_issue<UNS, NT>(A, A0, 0, lane, T, zero);
-    after_first_issue();
-    __builtin_amdgcn_sched_barrier(0); // keep the header wait behind the issue
-
-    PseudoHdr ph{0u, 1u, 0u};
-    if constexpr (PL) {
-        if (valid)
-            ph = hdr_pseudo(hdr, a);
-        if (__ballot(valid && !seg_payload_ok(a, len, ph))) {
-            done = false; // the caller takes the exact flat path
-            return 0;
-        }
-    }
-    done = true;
-    const uint32_t f1 = PL ? (ph.v4 ? 12u : 8u) : 0u;
-    const uint64_t rs = a + f1 - A0, re = a + len - A0;
+    const uint64_t rs = a + (PL ? 8u : 0u) - A0, re = a + len - A0;
     const uint32_t cs = (uint32_t)(rs >> 4), qs = (uint32_t)(rs & 15u);
     const uint32_t ce = (uint32_t)(re >> 4), qe = (uint32_t)(re & 15u);
+    const uint32_t c0 = (uint32_t)((a - A0) >> 4);
 
-    // payload_cksum, IPv4 with hl != 20: V of the bytes between 20 and hl
-    // (<= 40 bytes, <= 4 chunks), loaded by those lanes alone and summed
-    // before the stream goes on, so the chunks hold no registers across it.
-    const bool corr = PL && ph.v4 && ph.hl != 20u;
-    uint32_t cv = 0;
-    if constexpr (PL) {
-        if (__ballot(corr)) {
+    SegRows<UNS> A, B;
+    seg_issue<UNS, NT>(A, A0, 0, lane, T, zero);
+
+    uint32_t carry = 0, Ps = 0, Pe = 0;
+    u32x4 hs = {0u, 0u, 0u, 0u}, he = {0u, 0u, 0u, 0u}, h1 = {0u, 0u, 0u, 0u};
+    uint32_t j = 0;
+    for (; j < T; j += 2 * kGrp) {
+        seg_issue<UNS, NT>(B, A0, j + kGrp, lane, T, zero);
+        __builtin_amdgcn_sched_barrier(0);
+        seg_accum<UNS, PL>(A, pre, stage, j, lane, cs, ce, c0, carry, Ps, Pe, hs, he, h1);
+        __builtin_amdgcn_sched_barrier(0);
+        seg_issue<UNS, NT>(A, A0, j + 2 * kGrp, lane, T, zero);
+        __builtin_amdgcn_sched_barrier(0);
+        seg_accum<UNS, PL>(B, pre, stage, j + kGrp, lane, cs, ce, c0, carry, Ps, Pe, hs, he, h1);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    if (ce >= j) // the packet ends exactly at the last row group's end
+        Pe = carry;
+    done = true;
+    if constexpr (!PL) {
+        const uint32_t v = (Pe + seg_chunk<true>(he, qe)) - (Ps + seg_chunk<true>(hs, qs));
+        if (!(a & 1u))
+            return fold_not(v);
+        return fold_not(__builtin_amdgcn_alignbit(v, v, 24)); // rotl32(v, 8)
+    } else {
+        // Header bytes 0..11 from the packet's first two chunks (hs = c0, h1 =
+        // c0 + 1); the start chunk cs is one of them.
+        const uint32_t s = (uint32_t)(a & 15u);
+        const uint32_t w0 = win_bytes(hs, h1, s, 0), w1 = win_bytes(hs, h1, s, 1),
+                       w2 = win_bytes(hs, h1, s, 2);
+        const PseudoHdr ph = pseudo_hdr(w0 & 0xFFu, (w0 >> 16) & 0xFFu, w0 >> 24,
+                                        (w1 >> 16) & 0xFFu);
+        if (__ballot(valid && !seg_payload_ok(a, len, ph))) {
+            done = false;
+            return 0;
+        }
+        const u32x4 hq = cs == c0 ? hs : h1;
+        // V of [a + 8, a + len): IPv6 src/dst + body (hl = 40); IPv4 bytes
+        // 8..11, src/dst, options, body.
+        uint32_t v = (Pe + seg_chunk<true>(he, qe)) - (Ps + seg_chunk<true>(hq, qs));
+        const uint32_t odd = (uint32_t)(a & 1u);
+        if (ph.v4) {
+            // Minus bytes 8..11 (ttl, proto, header checksum), plus proto << 8
+            // (in_cksum.c:149) -- both at their address weight.
+            const uint32_t b9 = (w2 >> 8) & 0xFFu;
+            v -= wsum(odd ? __builtin_amdgcn_perm(w2, w2, 0x02030001u) : w2, 0u);
+            v += odd ? b9 : b9 << 8;
+        } else {
+            // plus the payload length word @4 (in_cksum.c:160)
+            const uint32_t b4 = w1 & 0xFFu, b5 = (w1 >> 8) & 0xFFu;
+            v += odd ? (b4 << 8) | b5 : b4 | (b5 << 8);
+        }
+        // IPv4 with hl != 20: the body starts at hl, not 20 -- minus the
+        // options [20, hl), or plus [hl, 20) (src/dst then count twice, as in
+        // the reference).  <= 40 bytes, <= 4 chunks, loaded by those lanes.
+        const bool corr = ph.v4 && ph.hl != 20u;
+        if (__ballot(valid && corr)) {
             const int clo = (int)min(ph.hl, 20u), chi = (int)max(ph.hl, 20u);
             const uint64_t ca = (a + (uint32_t)clo) & ~15ull;
             u32x4 xc[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                xc[k] = load_chunk<false>(corr && ca + 16ull * k < a + (uint32_t)chi
+                xc[k] = load_chunk<false>(valid && corr && ca + 16ull * k < a + (uint32_t)chi
                                               ? ca + 16ull * k : zero);
+            uint32_t cv = 0;
 #pragma unroll
             for (int k = 0; k < 4; ++k)
                 cv += seg_range(xc[k], (int)(ca - a) + 16 * k, clo, chi);
+            if (corr)
+                v = ph.hl < 20u ? v + cv : v - cv;
         }
-    }
-
-    uint32_t carry = 0, Ps = 0, Pe = 0;
-    u32x4 hs = {0u, 0u, 0u, 0u}, he = {0u, 0u, 0u, 0u};
-    uint32_t j = 0;
-    for (; j < T; j += 2 * kGrp) {
-        seg_issue<UNS, NT>(B, A0, j + kGrp, lane, T, zero);
-        __builtin_amdgcn_sched_barrier(0);
-        seg_accum<UNS>(A, pre, stage, j, lane, cs, ce, carry, Ps, Pe, hs, he);
-        __builtin_amdgcn_sched_barrier(0);
-        seg_issue<UNS, NT>(A, A0, j + 2 * kGrp, lane, T, zero);
-        __builtin_amdgcn_sched_barrier(0);
-        seg_accum<UNS>(B, pre, stage, j + kGrp, lane, cs, ce, carry, Ps, Pe, hs, he);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    if (ce >= j) // the packet ends exactly at the last row group's end
-        Pe = carry;
-
-    uint32_t v = (Pe + seg_chunk<true>(he, qe)) - (Ps + seg_chunk<true>(hs, qs));
-    if constexpr (PL) {
-        // Lone field bytes at their address weight: IPv4 proto @9 (odd
-        // offset), IPv6 payload length @4..5 (a word at an even offset).
-        const uint32_t odd = (uint32_t)(a & 1u);
-        const uint32_t h1 = hdr_h1(hdr, a);
-        const uint32_t b9 = (h1 >> 16) & 0xFFu, b4 = h1 & 0xFFu, b5 = (h1 >> 8) & 0xFFu;
-        v += ph.v4 ? (odd ? b9 : b9 << 8) : (odd ? (b4 << 8) | b5 : b4 | (b5 << 8));
-        // hl < 20: the body starts early (src/dst count twice, as in the
-        // reference); hl > 20: the options are not summed.
-        if (corr)
-            v = ph.hl < 20u ? v + cv : v - cv;
-    }
-    if (!(a & 1u))
-        return fold_not(v + ph.special); // exact, wrap included
-    const uint32_t r8 = __builtin_amdgcn_alignbit(v, v, 24); // rotl32(v, 8)
-    if constexpr (PL) {
-        // residue of r8 + special (no wrap: seg_wrap_risk), zero iff both are
-        const uint64_t t = (uint64_t)r8 + ph.special;
+        if (!odd)
+            return fold_not(v + ph.special); // exact, wrap included
+        // residue of rotl32(v, 8) + special (no wrap: seg_wrap_risk), zero
+        // iff both are
+        const uint64_t t = (uint64_t)__builtin_amdgcn_alignbit(v, v, 24) + ph.special;
         return fold_not((uint32_t)(t & 0xFFFFu) + (uint32_t)(t >> 16));
-    } else {
-        return fold_not(r8);
     }
 }
 
@@ -1257,20 +1290,21 @@ __device__ __forceinline__ void grp_accum(const GrpRows<UNG> &R, GrpAcc &S, GrpL
 // One uniform tile.  Returns this lane's packet's checksum, or done = false
 // (payload_cksum with a header longer than its packet: the caller takes the
 // flat path).
-template <int UNG, int KIND, bool NT, class F>
+template <int UNG, int KIND, bool NT>
 __device__ __forceinline__ uint16_t grp_tile(GrpLds &L, int lane, uint64_t a, uint32_t len,
-                                             bool valid, const HdrRaw &hdr, uint32_t Rq,
-                                             uint64_t zero, F &&after_first_issue, bool &done)
+                                             bool valid, uint32_t Rq, uint64_t zero, bool &done)
 {
-    // Addresses first: the first row group goes out before the header bytes
-    // are waited for.
+    // payload_cksum's header bytes: loaded first, waited for only after the
+    // first row group is issued (the addresses need no header).
+    HdrRaw hdr{};
+    if constexpr (KIND == WC_KIND_PAYLOAD)
+        hdr = load_hdr(a);
     L.gd[lane] = GrpDesc{(uint32_t)a, (uint32_t)(a >> 32), valid ? len : 0u, 0u};
     wave_order();
     GrpIssue I{0u, 0u, 0ull, 0u};
     grp_load_quad<KIND>(I, L, lane);
     GrpRows<UNG> A, B;
     grp_issue<UNG, KIND, NT>(A, I, L, lane, Rq, zero);
-    after_first_issue();
     __builtin_amdgcn_sched_barrier(0); // keep the header wait behind the issue
     if constexpr (KIND == WC_KIND_PAYLOAD) {
         PseudoHdr ph{0u, 1u, 0u};
@@ -1354,14 +1388,13 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     uint32_t nbad = 0;
     const uint64_t zero = (uint64_t)(uintptr_t)&kZeroChunk;
 
-    // Unconditional prefetch loads, as in k_cksum_flat.
+    // Unconditional metadata prefetch loads, as in k_cksum_flat.  No header
+    // prefetch: the seg path reads payload_cksum's header bytes out of its
+    // own stream, the grouped and flat paths load them when they run.
     uint64_t p = tile * 64 + lane;
     uint64_t off_n;
     uint32_t len_n;
     meta_load(offs, lens, p, n, off_n, len_n);
-    HdrRaw hdr_n{};
-    if constexpr (KIND == WC_KIND_PAYLOAD)
-        hdr_n = load_hdr((uint64_t)base + off_n);
 
     for (; tile < ntiles; tile += nwaves) {
         p = tile * 64 + lane;
@@ -1369,16 +1402,8 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
         const uint32_t nvalid = (uint32_t)min<uint64_t>(64, n - tile * 64);
         const uint64_t off = off_n;
         const uint32_t len = len_n;
-        const HdrRaw hdr = hdr_n;
         const uint64_t pn = (tile + nwaves) * 64 + lane;
         meta_load(offs, lens, pn, n, off_n, len_n);
-        bool prefetched = false;
-        auto prefetch_hdr = [&] {
-            if constexpr (KIND == WC_KIND_PAYLOAD)
-                if (!prefetched) // wave-uniform
-                    hdr_n = load_hdr((uint64_t)base + off_n);
-            prefetched = true;
-        };
 
         const uint64_t a = (uint64_t)base + off;
         uint64_t A0 = 0;
@@ -1394,19 +1419,18 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
         const bool grouped = Rq != 0 && (uint64_t)fill * 64u >= (uint64_t)thr * 1024u * Rq;
         bool done = false;
         if (grouped)
-            r = grp_tile<UNG, KIND, NT>(L.grp, lane, a, len, valid, hdr, Rq, zero, prefetch_hdr,
-                                        done);
+            r = grp_tile<UNG, KIND, NT>(L.grp, lane, a, len, valid, Rq, zero, done);
         else if (dense)
-            r = seg_tile<UNS, KIND, NT>(L.seg.pre, L.seg.stage, lane, a, len, valid, hdr, A0, T,
-                                        zero, prefetch_hdr, done);
+            r = seg_tile<UNS, KIND, NT>(L.seg.pre, L.seg.stage, lane, a, len, valid, A0, T, zero,
+                                        done);
         if (!done) {
             PseudoHdr ph{0u, 1u, 0u};
             if constexpr (KIND == WC_KIND_PAYLOAD)
                 if (valid)
-                    ph = hdr_pseudo(hdr, a);
+                    ph = hdr_pseudo(load_hdr(a), a);
             wave_order();
             r = fold_not(flat_tile_sum<UN, KIND, NT, false, true>(L.flat, nullptr, lane, a, len,
-                                                                  valid, ph, prefetch_hdr));
+                                                                  valid, ph, [] {}));
         }
         if (valid && out)
             out[p] = r;
