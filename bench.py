@@ -17,6 +17,10 @@ time reduction.
 --config c5 is SURVEY C5 (strong scaling): 2^28 x 1472 B in total, split
 evenly over the ranks; a rank whose share exceeds its resident window (2^25
 packets = 49 GB) checksums it as several launches over that window.
+--config slots is a netmap RX ring drained into one ragged batch
+(backend_netmap.c:379-391): 2^20 IP packets of --len + 28 B (1500 B) in
+2048-B buffers at +14 (eth.h:44-48), through wc_cksum_ragged; use it with
+--kind payload --headers for the RX verify pass of udp.c:132-139.
 
 Rank 0 prints ONE JSON line (see DESIGN.md section 6 for every field).
 """
@@ -45,7 +49,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5"])
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5", "slots"])
     ap.add_argument("--len", type=int, default=1472, help="packet bytes for c3")
     ap.add_argument("--kind", default="ip", choices=["ip", "payload"],
                     help="ip_cksum (default) or payload_cksum per packet")
@@ -137,6 +141,30 @@ def make_workload(args, dev, rank, world):
                 if args.config == "c2" else f"C3: {n} x {L} B packets, stride {L}")
         meta = {"packets_per_gpu": n, "packet_bytes": L, "layout": "strided", "kind": kind}
         return step, n, nbytes, buf, out, plan, desc, meta, (L, L), "weak"
+    if args.config == "slots":
+        n, L, slot, at = args.packets, args.len + 28, 2048, 14
+        offs = (np.arange(n, dtype=np.uint64) * slot + at).astype(np.uint64)
+        lens = np.full(n, L, dtype=np.uint16)
+        nbytes = n * L
+        buf = torch.empty(n * slot + 64, dtype=torch.uint8, device=dev)
+        wc.synth_fill(buf, seed, nbytes=n * slot)
+        d_off = torch.from_numpy(offs).to(dev)
+        d_len = torch.from_numpy(lens).to(dev)
+        if args.headers:
+            synth.stamp_udp_headers(buf, d_off, d_len)
+        out = torch.empty(n, dtype=torch.uint16, device=dev)
+
+        def step():
+            wc.cksum_ragged(buf, d_off, d_len, out=out, kind=kind)
+
+        desc = (f"netmap RX ring: {n} x {L} B IP packets in {slot}-B slots at +{at}, "
+                f"ragged batch")
+        meta = {"packets_per_gpu": n, "packet_bytes": L, "slot_bytes": slot,
+                "layout": "ragged", "kind": kind}
+        plan = {"kernel": "seg (grouped path for uniform tiles)",
+                "rows_per_group": int(os.environ.get("WC_GRP_ROWS", "4")),
+                "grid": int((n + 255) // 256)}
+        return step, n, nbytes, buf, out, plan, desc, meta, (offs, lens), "weak"
     # C4: Zipf(1) lengths 64..1472 B, packed with no padding (unaligned starts)
     n = 1 << 24 if args.packets == (1 << 20) else args.packets
     lens = synth.zipf_lengths(n, seed=synth.ZIPF_SEED + rank)
@@ -187,7 +215,7 @@ def cpu_baseline(args, buf, shape, nbytes_total):
     else:
         offs, lens = shape
         n_s = min(offs.size, 1 << 22)
-        end = int(offs[n_s - 1]) + int(lens[n_s - 1])
+        end = int(offs[n_s - 1]) + max(int(lens[n_s - 1]), 40)
         sample = buf[:end].cpu().numpy()
         t0 = time.perf_counter()
         passes = 0
@@ -197,7 +225,8 @@ def cpu_baseline(args, buf, shape, nbytes_total):
             if time.perf_counter() - t0 >= args.cpu_seconds:
                 break
         bps = passes * float(lens[:n_s].astype(np.uint64).sum()) / (time.perf_counter() - t0)
-        desc = f"first {n_s} Zipf packets ({end / 1e6:.0f} MB), {passes} passes"
+        desc = (f"first {n_s} {'Zipf ' if args.config == 'c4' else ''}packets "
+                f"({end / 1e6:.0f} MB), {passes} passes")
     try:
         model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo")
                      if l.startswith("model name"))
@@ -223,7 +252,11 @@ def parity_check(args, buf, out, shape, nbytes):
     from oracle import c_oracle
     k = 1 if args.kind == "payload" else 0
     got = out.cpu().numpy().view(np.uint16)
-    hb = buf[: got.size * shape[1] if args.config != "c4" else nbytes].cpu().numpy()
+    if args.config in ("c2", "c3", "c5"):
+        hb = buf[: got.size * shape[1]].cpu().numpy()
+    else:  # ragged: every byte up to the last packet's end (+ its header fields)
+        offs, lens = shape
+        hb = buf[: min(buf.numel(), int(offs[-1]) + max(int(lens[-1]), 40))].cpu().numpy()
     if args.config in ("c2", "c3", "c5"):
         # c5: the last launch of the step covered the window's first
         # `counts[-1]` packets; check the whole window result of that launch
@@ -285,6 +318,8 @@ def main():
         key = f"{args.config}:{meta.get('packet_bytes', 'zipf')}"
         if args.kind != "ip":
             key += f":{args.kind}"
+        if args.headers:
+            key += ":headers"
         if key in tf:
             traffic = tf[key]["hbm_bytes_per_launch"]
     except (OSError, ValueError, KeyError):

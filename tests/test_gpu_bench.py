@@ -52,3 +52,21 @@ def test_bench_two_ranks_rehearsal(gpu):
     assert line["n_gpus"] == 2 and line["scaling"] == "weak"
     assert line["cpu_baseline"] is None
     assert line["parity"] == {"checked_packets": 2 * 65536, "mismatches": 0}
+
+
+@pytest.mark.parametrize("args", [["--config", "c4", "--packets", "200000"],
+                                  ["--config", "c4", "--packets", "200000", "--kind", "payload",
+                                   "--headers"],
+                                  ["--config", "slots", "--packets", "65536", "--kind", "payload",
+                                   "--headers"],
+                                  ["--config", "c2", "--packets", "65536", "--kind", "payload"]])
+def test_bench_other_configs(gpu, args):
+    """The secondary bench lines (C4, payload_cksum, the netmap RX-ring layout)
+    stay runnable and bit-exact."""
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--steps", "3", "--warmup", "1",
+                        "--cpu-seconds", "0.2", *args],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = _last_json(r.stdout)
+    assert line["value"] > 0 and line["parity"]["mismatches"] == 0
+    assert line["parity"]["checked_packets"] == line["config"]["packets_per_gpu"]
