@@ -296,12 +296,40 @@ __device__ __forceinline__ void accum_strided(const u32x4 &d, int co, int rs, in
     }
 }
 
+__device__ __forceinline__ uint32_t lane_u32(uint32_t v, int l)
+{
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+
+// DPP move with every source lane valid (quad_perm / mirror patterns).
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_all(uint32_t v)
+{
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+
+// Sum over each aligned group of G lanes (mod 2^32), in every lane of the
+// group.  DPP within a 16-lane row (quad_perm xor 1 / xor 2, row_half_mirror,
+// row_mirror), readlane across rows: no LDS round trips (ds_bpermute), which
+// dominated the small-packet shapes' per-packet cost.
 template <int G>
 __device__ __forceinline__ uint32_t group_sum(uint32_t v)
 {
-#pragma unroll
-    for (int m = G / 2; m >= 1; m >>= 1)
-        v += __shfl_xor(v, m, 64);
+    if constexpr (G >= 2)
+        v += dpp_all<0xB1>(v); // quad_perm [1,0,3,2]
+    if constexpr (G >= 4)
+        v += dpp_all<0x4E>(v); // quad_perm [2,3,0,1]
+    if constexpr (G >= 8)
+        v += dpp_all<0x141>(v); // row_half_mirror: the other quad of the 8
+    if constexpr (G >= 16)
+        v += dpp_all<0x140>(v); // row_mirror: the other half of the row
+    if constexpr (G == 32) {
+        const uint32_t lo = lane_u32(v, 0) + lane_u32(v, 16);
+        const uint32_t hi = lane_u32(v, 32) + lane_u32(v, 48);
+        v = (threadIdx.x & 32) ? hi : lo;
+    } else if constexpr (G == 64) {
+        v = lane_u32(v, 0) + lane_u32(v, 16) + lane_u32(v, 32) + lane_u32(v, 48);
+    }
     return v;
 }
 
@@ -445,9 +473,7 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
 
     if (bad) {
         // Wave-level total of the leaders' counts, one atomic per wave.
-#pragma unroll
-        for (int m = 32; m >= 1; m >>= 1)
-            nbad += __shfl_xor(nbad, m, 64);
+        nbad = group_sum<64>(nbad);
         if (lane == 0 && nbad)
             atomicAdd(bad, (unsigned long long)nbad);
     }
@@ -508,11 +534,7 @@ __device__ __forceinline__ uint32_t mbcnt64(uint64_t m)
 }
 
 // Wave-uniform broadcasts and shifts without LDS round trips (readlane /
-// DPP instead of ds_bpermute).
-__device__ __forceinline__ uint32_t lane_u32(uint32_t v, int l)
-{
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
-}
+// DPP instead of ds_bpermute); lane_u32 is defined with group_sum.
 
 __device__ __forceinline__ uint64_t lane_u64(uint64_t v, int l)
 {
@@ -861,9 +883,7 @@ k_cksum_flat(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
         wave_order(); // the tables are rewritten by the next tile
     }
     if (bad) {
-#pragma unroll
-        for (int m = 32; m >= 1; m >>= 1)
-            nbad += __shfl_xor(nbad, m, 64);
+        nbad = group_sum<64>(nbad);
         if (lane == 0 && nbad)
             atomicAdd(bad, (unsigned long long)nbad);
     }
@@ -1438,9 +1458,7 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
         wave_order(); // the tables are rewritten by the next tile
     }
     if (bad) {
-#pragma unroll
-        for (int m = 32; m >= 1; m >>= 1)
-            nbad += __shfl_xor(nbad, m, 64);
+        nbad = group_sum<64>(nbad);
         if (lane == 0 && nbad)
             atomicAdd(bad, (unsigned long long)nbad);
     }
