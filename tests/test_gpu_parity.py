@@ -120,6 +120,38 @@ def test_strided_sweep(gpu, length):
             np.testing.assert_array_equal(got, want, err_msg=f"stride {stride} start {start}")
 
 
+@pytest.mark.parametrize("sseg", ["0", "1", "2"])
+@pytest.mark.parametrize("length", [1, 2, 15, 16, 17, 63, 64, 65, 100, 111, 128, 255, 256, 257,
+                                    576, 577, 767, 768, 1472, 1500, 9000])
+def test_strided_packed_seg(gpu, monkeypatch, length, sseg):
+    """Packed strided batches (stride = len .. len + len / 8) through the seg
+    kernel with computed offsets (WC_STRIDED_SEG: 0 = group kernel only,
+    1 = planner default, 2 = seg kernel whenever packed): several tiles and
+    a partial one, every start phase, ip_cksum and payload_cksum."""
+    monkeypatch.setenv("WC_STRIDED_SEG", sseg)
+    rng = np.random.default_rng(length * 7 + int(sseg))
+    n = 150
+    for stride in sorted({length, length + 1, length + length // 8}):
+        buf = rng.integers(0, 256, n * stride + 64 + 16, dtype=np.uint8)
+        d = dev_u8(buf, gpu)
+        for start in (0, 1, 6, 14, 15):
+            got = host(wc.cksum_strided(d, stride, length, n, kind="ip", byte_offset=start))
+            want = c_oracle.cksum_strided(buf, stride, length, n, kind=0, byte_offset=start)
+            np.testing.assert_array_equal(got, want, err_msg=f"ip stride {stride} start {start}")
+        if length >= 48:  # payload_cksum: well-formed UDP headers, then the RX check
+            hb = buf.copy()
+            for i in range(n):
+                o = 14 + i * stride
+                pl = rng.integers(0, 256, length - 28 - (20 if i % 3 == 0 else 0),
+                                  dtype=np.uint8).tobytes()
+                pkt, ln = (ipv6_udp if i % 3 == 0 else ipv4_udp)(pl, rng)
+                hb[o:o + ln] = np.frombuffer(pkt, np.uint8)
+            d = dev_u8(hb, gpu)
+            got = host(wc.cksum_strided(d, stride, length, n, kind="payload", byte_offset=14))
+            want = c_oracle.cksum_strided(hb, stride, length, n, kind=1, byte_offset=14)
+            np.testing.assert_array_equal(got, want, err_msg=f"payload stride {stride}")
+
+
 @pytest.mark.parametrize("mode", list(RAGGED_MODES))
 def test_ragged_random_placement(gpu, monkeypatch, mode):
     ragged_mode(monkeypatch, mode)

@@ -169,7 +169,9 @@ wc::Shape shape_for_chunks(uint32_t nch)
     // group so every lane keeps ~4-18 16-byte loads in flight (tuned on
     // MI355X: DESIGN.md section 5, profiles/tune_r01_*.log).
     if (nch <= 4)
-        return {4, 1, 8};
+        return {4, 1, 4};
+    if (nch <= 6)
+        return {4, 2, 2};
     if (nch <= 8)
         return {8, 1, 4};
     if (nch <= 16)
@@ -226,7 +228,7 @@ struct Plan {
 };
 
 Plan plan_strided(const Device &D, uint64_t base, uint64_t stride, uint32_t len,
-                  uint64_t n, int kind)
+                  uint64_t n, int kind, bool hdr = false)
 {
     Plan p;
     const uint32_t span = kind == WC_CKSUM_PAYLOAD ? std::max(len, 20u) : len;
@@ -238,6 +240,22 @@ Plan plan_strided(const Device &D, uint64_t base, uint64_t stride, uint32_t len,
     p.full = kind == WC_CKSUM_IP && base % 16 == 0 && stride % 16 == 0 &&
              len % 16 == 0 && !(env_int("WC_VARIANT", 0) & 2);
     p.grid = grid_for(D, p.shape, n);
+    // Packed (or nearly packed) packets that the group kernel would have to
+    // mask: the seg kernel streams their byte range instead (k_cksum_seg<STR>)
+    // -- measured better from 7 to 48 chunks per packet (256 B at +14: 59 ->
+    // 78 % of HBM peak, 576 B at +14: 77 -> 83 %), worse at MTU size (88 ->
+    // 85 %) and for tiny packets.  WC_STRIDED_SEG = 0
+    // never, 2 always (no fused header), 1 = chunk counts in
+    // [WC_STRIDED_SEG_MINCH, WC_STRIDED_SEG_MAXCH].
+    const int sseg = env_int("WC_STRIDED_SEG", 1);
+    const bool packed = len != 0 && stride >= len && stride <= len + len / 8u;
+    const bool seg_size = nch >= (uint32_t)env_int("WC_STRIDED_SEG_MINCH", 7) &&
+                          nch <= (uint32_t)env_int("WC_STRIDED_SEG_MAXCH", 48);
+    if (!hdr && !p.full && n >= 64 && packed && (sseg == 2 || (sseg == 1 && seg_size))) {
+        p.shape = {0, 1, env_int("WC_FLAT_UN", 2)};
+        p.seg_rows = env_int("WC_SEG_ROWS", 4);
+        p.grid = 0;
+    }
     return p;
 }
 
@@ -305,7 +323,7 @@ int batch_strided(const void *d_base, uint64_t stride, uint16_t len, uint64_t n,
     int rc = ensure_device(&D);
     if (rc)
         return rc;
-    const Plan p = plan_strided(*D, (uint64_t)d_base, stride, len, n, kind);
+    const Plan p = plan_strided(*D, (uint64_t)d_base, stride, len, n, kind, d_out_hdr != nullptr);
     wc::LaunchArgs a{d_base, stride, len,  nullptr,  nullptr, n,
                      d_out,  d_bad,  kind, false,    p.full,  nontemporal(),
                      0,      d_out_hdr};

@@ -13,7 +13,14 @@
 // WC_SHAPE may request; each is instantiated for ip_cksum (masked and
 // aligned-unmasked) and payload_cksum, with temporal and nontemporal loads.
 #define WC_SHAPE_LIST                                                          \
+    WC_SHAPE(4, 1, 2)                                                          \
+    WC_SHAPE(4, 1, 4)                                                          \
     WC_SHAPE(4, 1, 8)                                                          \
+    WC_SHAPE(4, 2, 2)                                                          \
+    WC_SHAPE(4, 2, 4)                                                          \
+    WC_SHAPE(8, 1, 2)                                                          \
+    WC_SHAPE(8, 2, 4)                                                          \
+    WC_SHAPE(16, 1, 2)                                                         \
     WC_SHAPE(4, 1, 16)                                                         \
     WC_SHAPE(8, 1, 4)                                                          \
     WC_SHAPE(8, 1, 8)                                                          \

@@ -1381,12 +1381,16 @@ __device__ __forceinline__ bool seg_dense(int lane, uint64_t a, uint32_t len, bo
 
 // Ragged kernel with both paths: dense tiles stream their byte range
 // (seg_tile), the others take the flat path.  (The fused header checksum
-// stays on k_cksum_flat.)
-template <int UN, int UNS, int UNG, int KIND, bool NT>
+// stays on k_cksum_flat.)  STR: a strided batch (packet i at i * stride,
+// slen bytes) -- packed packets at any alignment are one dense byte range,
+// which the seg path streams better than the group kernel masks its
+// boundary chunks; offsets and lengths are computed, not loaded.
+template <int UN, int UNS, int UNG, int KIND, bool NT, bool STR>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UNS >= 8 ? 2 : 4)))
 k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
             const uint16_t *__restrict__ lens, uint64_t n, uint16_t *__restrict__ out,
-            unsigned long long *__restrict__ bad, int grp_thr, int variant)
+            unsigned long long *__restrict__ bad, int grp_thr, int variant, uint64_t stride,
+            uint32_t slen)
 {
     (void)variant; // WC_VARIANT: A/B experiments
     union TileLds {
@@ -1411,10 +1415,18 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     // Unconditional metadata prefetch loads, as in k_cksum_flat.  No header
     // prefetch: the seg path reads payload_cksum's header bytes out of its
     // own stream, the grouped and flat paths load them when they run.
+    auto meta = [&](uint64_t q, uint64_t &off, uint32_t &len) {
+        if constexpr (STR) {
+            off = (q < n ? q : 0) * stride;
+            len = q < n ? slen : 0u;
+        } else {
+            meta_load(offs, lens, q, n, off, len);
+        }
+    };
     uint64_t p = tile * 64 + lane;
     uint64_t off_n;
     uint32_t len_n;
-    meta_load(offs, lens, p, n, off_n, len_n);
+    meta(p, off_n, len_n);
 
     for (; tile < ntiles; tile += nwaves) {
         p = tile * 64 + lane;
@@ -1423,7 +1435,7 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
         const uint64_t off = off_n;
         const uint32_t len = len_n;
         const uint64_t pn = (tile + nwaves) * 64 + lane;
-        meta_load(offs, lens, pn, n, off_n, len_n);
+        meta(pn, off_n, len_n);
 
         const uint64_t a = (uint64_t)base + off;
         uint64_t A0 = 0;
@@ -1574,15 +1586,26 @@ static hipError_t launch_flat_un(const LaunchArgs &a, hipStream_t st)
         return hipGetLastError();
     }
     if (a.seg_rows && !a.out_hdr) {
-#define WC_SEG(US, UG)                                                         \
-    if (a.kind == WC_KIND_PAYLOAD)                                             \
-        hipLaunchKernelGGL((k_cksum_seg<UN, US, UG, WC_KIND_PAYLOAD, true>), dim3(grid), \
-                           dim3(256), 0, st, b, a.offs, a.lens, a.n, a.out, bad, a.grp_thr, \
-                           a.variant);                                         \
-    else                                                                       \
-        hipLaunchKernelGGL((k_cksum_seg<UN, US, UG, WC_KIND_IP, true>), dim3(grid), \
-                           dim3(256), 0, st, b, a.offs, a.lens, a.n, a.out, bad, a.grp_thr, \
-                           a.variant);
+#define WC_SEG_K(K, S)                                                         \
+    hipLaunchKernelGGL((k_cksum_seg<UN, US, UG, K, true, S>), dim3(grid), dim3(256), 0, st, \
+                       b, a.offs, a.lens, a.n, a.out, bad, a.grp_thr, a.variant, a.stride, \
+                       a.len)
+#define WC_SEG(US_, UG_)                                                       \
+    {                                                                          \
+        constexpr int US = US_, UG = UG_;                                      \
+        const bool str = a.offs == nullptr;                                    \
+        if (a.kind == WC_KIND_PAYLOAD) {                                       \
+            if (str)                                                           \
+                WC_SEG_K(WC_KIND_PAYLOAD, true);                               \
+            else                                                               \
+                WC_SEG_K(WC_KIND_PAYLOAD, false);                              \
+        } else {                                                               \
+            if (str)                                                           \
+                WC_SEG_K(WC_KIND_IP, true);                                    \
+            else                                                               \
+                WC_SEG_K(WC_KIND_IP, false);                                   \
+        }                                                                      \
+    }
         // Row-group sizes: seg path a.seg_rows (WC_SEG_ROWS), grouped path
         // a.grp_rows (WC_GRP_ROWS 4 or 2, with the default flat and seg
         // sizes only; 6 and 8 measured no faster on netmap slots).
@@ -1596,6 +1619,7 @@ static hipError_t launch_flat_un(const LaunchArgs &a, hipStream_t st)
             WC_SEG(4, 2)
         }
 #undef WC_SEG
+#undef WC_SEG_K
         return hipGetLastError();
     }
     if (a.kind == WC_KIND_PAYLOAD && a.out_hdr) {
