@@ -608,14 +608,49 @@ def _ip_hdr_expect(buf: np.ndarray, offs, lens) -> np.ndarray:
     return np.array([py_oracle.ip_hdr_cksum(b[int(o):int(o) + 64]) for o in offs], np.uint16)
 
 
+@pytest.mark.parametrize("mode", list(RAGGED_MODES))
 @pytest.mark.parametrize("align,lead", [(1, 0), (2, 14), (16, 0), (1, 5)])
-def test_fused_ip_udp_ragged(gpu, align, lead):
+def test_fused_ip_udp_ragged(gpu, monkeypatch, align, lead, mode):
+    ragged_mode(monkeypatch, mode)
     rng = np.random.default_rng(200 + align + lead)
     pkts = random_packets(rng, 2500, max_payload=1472, wild=True)
     buf, offs, lens = pack(pkts, align=align, lead=lead)
     hdr, pay = wc.cksum_ip_udp_ragged(dev_u8(buf, gpu), to_dev(offs, gpu), to_dev(lens, gpu))
     np.testing.assert_array_equal(host(pay), c_oracle.cksum_ragged(buf, offs, lens, kind=1))
     np.testing.assert_array_equal(host(hdr), _ip_hdr_expect(buf, offs, lens))
+
+
+@pytest.mark.parametrize("mode", list(RAGGED_MODES))
+@pytest.mark.parametrize("align", [1, 2])
+def test_fused_ip_udp_malformed(gpu, monkeypatch, align, mode):
+    """The fused pass over random bytes read as IP packets (every IHL, both
+    versions, len == hl) in packed tiles and netmap-like uniform slots: both
+    checksums of every packet against the oracle."""
+    ragged_mode(monkeypatch, mode)
+    rng = np.random.default_rng(41 + align)
+    pkts = []
+    for i in range(3000):
+        ln = int(rng.integers(0, 120)) if i % 3 else int(rng.integers(1000, 1501))
+        b = bytearray(rng.integers(0, 256, 40, dtype=np.uint8).tobytes())
+        b[0] = (0x40 | int(rng.integers(0, 16))) if rng.random() < 0.6 else (0x60 | 5)
+        hl = (b[0] & 15) * 4 if b[0] >> 4 == 4 else 40
+        ln = max(ln, hl)  # len < hl: the reference reads ~4 GiB (undefined)
+        pkts.append((bytes(b) + rng.integers(0, 256, max(ln, 40) - 40, dtype=np.uint8).tobytes(),
+                     ln))
+    buf, offs, lens = pack(pkts, align=align, lead=3)
+    hdr, pay = wc.cksum_ip_udp_ragged(dev_u8(buf, gpu), to_dev(offs, gpu), to_dev(lens, gpu))
+    np.testing.assert_array_equal(host(pay), c_oracle.cksum_ragged(buf, offs, lens, kind=1))
+    np.testing.assert_array_equal(host(hdr), _ip_hdr_expect(buf, offs, lens))
+    # the same packets spread over 2048-B slots at +14 (uniform-length tiles)
+    big = [(p, l) for p, l in pkts if l >= 1000]
+    slots = np.zeros(len(big) * 2048 + 64, np.uint8)
+    so = np.arange(len(big), dtype=np.uint64) * 2048 + 14
+    for (pk, _), o in zip(big, so.tolist()):
+        slots[o:o + len(pk)] = np.frombuffer(pk, np.uint8)
+    sl = np.array([l for _, l in big], np.uint16)
+    hdr, pay = wc.cksum_ip_udp_ragged(dev_u8(slots, gpu), to_dev(so, gpu), to_dev(sl, gpu))
+    np.testing.assert_array_equal(host(pay), c_oracle.cksum_ragged(slots, so, sl, kind=1))
+    np.testing.assert_array_equal(host(hdr), _ip_hdr_expect(slots, so, sl))
 
 
 @pytest.mark.parametrize("v6", [False, True])
@@ -637,10 +672,12 @@ def test_fused_ip_udp_strided_netmap(gpu, v6):
     np.testing.assert_array_equal(host(hdr), _ip_hdr_expect(buf, offs, None))
 
 
-def test_fused_tx_then_rx_roundtrip(gpu):
+@pytest.mark.parametrize("mode", list(RAGGED_MODES))
+def test_fused_tx_then_rx_roundtrip(gpu, monkeypatch, mode):
     """TX: header and UDP checksums computed with both fields 0 (ip4.c:184-186,
     udp.c:209-213) and stored raw; RX: the same pass over the stored packets
     gives 0 for both (ip4.c:110-115, udp.c:132-139)."""
+    ragged_mode(monkeypatch, mode)
     rng = np.random.default_rng(23)
     pkts = [(p, l) for p, l in random_packets(rng, 1500, max_payload=1400, v6_share=0.3)]
     buf, offs, lens = pack(pkts, align=2, lead=14)

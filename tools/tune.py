@@ -67,6 +67,8 @@ def main():
     ap.add_argument("--kind", default="ip", choices=["ip", "payload"])
     ap.add_argument("--offset", type=int, default=0, help="byte offset of packet 0 (c2/c3)")
     ap.add_argument("--stride", type=int, default=0, help="packet stride (c2/c3; default len)")
+    ap.add_argument("--fused", action="store_true",
+                    help="fused IPv4 header + payload_cksum pass (wc_cksum_ip_udp_*)")
     ap.add_argument("--headers", action="store_true",
                     help="well-formed IPv4 / IPv6 UDP headers (synth.stamp_udp_headers)")
     ap.add_argument("--ragged", action="store_true",
@@ -88,6 +90,8 @@ def main():
             synth.stamp_udp_headers(buf, d_off, d_len)
         out = torch.empty(n, dtype=torch.uint16, device=dev)
         run = lambda: wc.cksum_ragged(buf, d_off, d_len, out=out, kind=args.kind)  # noqa: E731
+        if args.fused:
+            run = lambda: wc.cksum_ip_udp_ragged(buf, d_off, d_len)  # noqa: E731
     else:
         L = 1472 if args.config == "c2" else args.len
         n = args.packets
@@ -101,10 +105,15 @@ def main():
         out = torch.empty(n, dtype=torch.uint16, device=dev)
         run = lambda: wc.cksum_strided(buf, stride, L, n, out=out, kind=args.kind,  # noqa: E731
                                        byte_offset=args.offset)
+        if args.fused:
+            run = lambda: wc.cksum_ip_udp_strided(buf, stride, L, n,  # noqa: E731
+                                                  byte_offset=args.offset)
         if args.ragged:
             d_off = torch.arange(n, dtype=torch.int64, device=dev) * stride + args.offset
             d_len = torch.full((n,), L, dtype=torch.int16, device=dev)
             run = lambda: wc.cksum_ragged(buf, d_off, d_len, out=out, kind=args.kind)  # noqa: E731
+            if args.fused:
+                run = lambda: wc.cksum_ip_udp_ragged(buf, d_off, d_len)  # noqa: E731
 
     variants = [("" if v.strip() == "default" else v.strip()) for v in args.variants.split(";") if v.strip()] or [""]
     # Every WC_* knob a variant may set is reset before the next variant runs.

@@ -261,10 +261,10 @@ Plan plan_strided(const Device &D, uint64_t base, uint64_t stride, uint32_t len,
 
 // Ragged batches take the segmented-prefix kernel k_cksum_seg (both kinds):
 // dense tiles stream their byte range, sparse ones take its flat path
-// (DESIGN.md section 4.3).  The fused header pass (out_hdr) takes the
-// chunk-balanced flat kernel (group = 0 marks both; unroll = 64-chunk rows
-// per ping-pong group, WC_FLAT_UN).  WC_SEG = 0 forces the flat kernel;
-// WC_SEG_ROWS = 2 / 4 / 8 rows per seg row group.  A host zero-copy batch of
+// (DESIGN.md section 4.4), the fused header pass (out_hdr) included (group =
+// 0 marks both the seg and the flat kernel; unroll = 64-chunk rows per
+// ping-pong group of the flat path, WC_FLAT_UN).  WC_SEG = 0 forces the flat
+// kernel; WC_SEG_ROWS = 2 / 4 / 8 rows per seg row group.  A host zero-copy batch of
 // at most kZcGroupMax packets takes the ragged group kernel instead: a flat
 // wave walks its 64-packet tile's rows one PCIe latency at a time, the group
 // kernel issues every packet's loads at once.  (Device-resident batches
@@ -288,8 +288,8 @@ Plan plan_ragged(const Device &D, uint64_t n, int kind, bool zero_copy = false,
     p.shape = {0, 1, env_int("WC_FLAT_UN", 2)};
     p.grid = 0;
     const int seg = env_int("WC_SEG", 1);
-    (void)kind;
-    if (!hdr && !zero_copy && env_int("WC_DIAG_NOLOAD", 0) == 0 && seg != 0)
+    if (!zero_copy && env_int("WC_DIAG_NOLOAD", 0) == 0 && seg != 0 &&
+        (!hdr || kind == WC_CKSUM_PAYLOAD))
         p.seg_rows = env_int("WC_SEG_ROWS", 4);
     return p;
 }

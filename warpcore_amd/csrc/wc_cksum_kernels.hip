@@ -731,7 +731,7 @@ __device__ __forceinline__ PseudoHdr hdr_pseudo(const HdrRaw &h, uint64_t a)
 // its header [0, hl) (at most 5 chunks) -- ip_cksum(ip, hl), ip4.c:110-115.
 template <bool NT>
 __device__ __forceinline__ uint16_t lane_hdr_cksum(uint64_t a, uint32_t hl,
-                                                   const WeightLut &M)
+                                                   const WeightLut *M)
 {
     const uint32_t s = (uint32_t)(a & 15u);
     const uint64_t c0 = a & ~15ull;
@@ -740,7 +740,10 @@ __device__ __forceinline__ uint16_t lane_hdr_cksum(uint64_t a, uint32_t hl,
     for (uint32_t k = 0; k < nh; ++k) {
         const u32x4 d = load_chunk<false>(c0 + 16ull * k);
         const int co = (int)(16u * k) - (int)s;
-        accum_masked<WC_KIND_IP>(d, co, 0, (int)hl, 0u, M, E, O);
+        if (M) // the flat kernel's LDS tables, or arithmetic masks
+            accum_masked<WC_KIND_IP>(d, co, 0, (int)hl, 0u, *M, E, O);
+        else
+            accum_arith<WC_KIND_IP>(d, co, 0, (int)hl, 0u, E, O);
     }
     return fold_not(combine(E, O, s & 1u));
 }
@@ -879,7 +882,7 @@ k_cksum_flat(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
         nbad += valid && r != 0;
         if constexpr (HDR)
             if (valid)
-                out_hdr[p] = ph.v4 ? lane_hdr_cksum<NT>(a, ph.hl, lut) : 0;
+                out_hdr[p] = ph.v4 ? lane_hdr_cksum<NT>(a, ph.hl, &lut) : 0;
         wave_order(); // the tables are rewritten by the next tile
     }
     if (bad) {
@@ -992,14 +995,16 @@ __device__ __forceinline__ void seg_issue(SegRows<UNS> &R, uint64_t A0, uint32_t
 // Sum the UNS rows of the group at slot g0: row prefix sums (DPP), chained
 // through LDS; packet lanes whose start / end chunk falls in the group pick
 // up the running sum before it and the chunk itself.  `carry` is the running
-// sum before the group (wave-uniform).  With HC (payload_cksum) the lane also
-// picks up its packet's first two chunks c0, c0 + 1 -- its header bytes
-// 0..11, and the start chunk cs, which is one of them.
-template <int UNS, bool HC>
+// sum before the group (wave-uniform).  With HC >= 2 (payload_cksum) the lane
+// also picks up its packet's first HC chunks c0, c0 + 1 (, c0 + 2) -- its
+// header bytes 0..11 (0..19 with the fused header checksum), and the start
+// chunk cs, which is c0 or c0 + 1.
+template <int UNS, int HC>
 __device__ __forceinline__ void seg_accum(const SegRows<UNS> &R, uint32_t *pre, u32x4 *stage,
                                           uint32_t g0, int lane, uint32_t cs, uint32_t ce,
                                           uint32_t c0, uint32_t &carry, uint32_t &Ps,
-                                          uint32_t &Pe, u32x4 &hs, u32x4 &he, u32x4 &h1)
+                                          uint32_t &Pe, u32x4 &hs, u32x4 &he, u32x4 &h1,
+                                          u32x4 &h2)
 {
     constexpr uint32_t kGrp = 64u * UNS;
     uint32_t P[UNS];
@@ -1027,12 +1032,15 @@ __device__ __forceinline__ void seg_accum(const SegRows<UNS> &R, uint32_t *pre, 
     const uint32_t ds = cs - g0, de = ce - g0;
     // The packet's first / last chunk, for its partial sums (exec-masked
     // LDS reads: no scattered global re-loads).
-    if constexpr (HC) {
+    if constexpr (HC >= 2) {
         const uint32_t d0 = c0 - g0; // (unsigned: c0 + 1 == g0 gives d0 + 1 == 0)
         if (d0 < kGrp)
             hs = stage[d0];
         if (d0 + 1u < kGrp)
             h1 = stage[d0 + 1u];
+        if constexpr (HC >= 3)
+            if (d0 + 2u < kGrp)
+                h2 = stage[d0 + 2u];
     } else {
         if (ds < kGrp)
             hs = stage[ds];
@@ -1049,20 +1057,21 @@ __device__ __forceinline__ void seg_accum(const SegRows<UNS> &R, uint32_t *pre, 
     wave_order(); // pre is rewritten by the next group
 }
 
-// Dword k (0..7) of the 32-byte window x:y.
-__device__ __forceinline__ uint32_t win_dword(const u32x4 &x, const u32x4 &y, uint32_t k)
+// Dword k (0..11) of the 48-byte window x:y:z.
+__device__ __forceinline__ uint32_t win_dword(const u32x4 &x, const u32x4 &y, const u32x4 &z,
+                                              uint32_t k)
 {
-    const u32x4 &h = k & 4u ? y : x;
+    const u32x4 &h = k >= 8u ? z : (k & 4u ? y : x);
     return pick_dword(h, (int)(k & 3u));
 }
 
-// Packet bytes 4 m .. 4 m + 3 from the window x:y that holds the packet's
+// Packet bytes 4 m .. 4 m + 3 from the window x:y:z that holds the packet's
 // first bytes from offset s on.
-__device__ __forceinline__ uint32_t win_bytes(const u32x4 &x, const u32x4 &y, uint32_t s,
-                                              uint32_t m)
+__device__ __forceinline__ uint32_t win_bytes(const u32x4 &x, const u32x4 &y, const u32x4 &z,
+                                              uint32_t s, uint32_t m)
 {
     const uint32_t k = (s >> 2) + m;
-    return __builtin_amdgcn_alignbit(win_dword(x, y, k + 1u), win_dword(x, y, k),
+    return __builtin_amdgcn_alignbit(win_dword(x, y, z, k + 1u), win_dword(x, y, z, k),
                                      8u * (s & 3u));
 }
 
@@ -1089,13 +1098,14 @@ __device__ __forceinline__ bool seg_payload_ok(uint64_t a, uint32_t len, const P
 // the checksum, or done = false when a payload_cksum lane can't be summed
 // here (header longer than the packet, possible uint32 wrap): the caller
 // then takes the exact flat path for the tile.
-template <int UNS, int KIND, bool NT>
+template <int UNS, int KIND, bool NT, bool HDR>
 __device__ __forceinline__ uint16_t seg_tile(uint32_t *pre, u32x4 *stage, int lane, uint64_t a,
                                              uint32_t len, bool valid, uint64_t A0, uint32_t T,
-                                             uint64_t zero, bool &done)
+                                             uint64_t zero, bool &done, uint16_t &rh)
 {
     constexpr uint32_t kGrp = 64u * UNS;
     constexpr bool PL = KIND == WC_KIND_PAYLOAD;
+    constexpr int HC = PL ? (HDR ? 3 : 2) : 0;
     const uint64_t rs = a + (PL ? 8u : 0u) - A0, re = a + len - A0;
     const uint32_t cs = (uint32_t)(rs >> 4), qs = (uint32_t)(rs & 15u);
     const uint32_t ce = (uint32_t)(re >> 4), qe = (uint32_t)(re & 15u);
@@ -1105,16 +1115,18 @@ __device__ __forceinline__ uint16_t seg_tile(uint32_t *pre, u32x4 *stage, int la
     seg_issue<UNS, NT>(A, A0, 0, lane, T, zero);
 
     uint32_t carry = 0, Ps = 0, Pe = 0;
-    u32x4 hs = {0u, 0u, 0u, 0u}, he = {0u, 0u, 0u, 0u}, h1 = {0u, 0u, 0u, 0u};
+    u32x4 hs = {0u, 0u, 0u, 0u}, he = {0u, 0u, 0u, 0u}, h1 = {0u, 0u, 0u, 0u},
+          h2 = {0u, 0u, 0u, 0u};
     uint32_t j = 0;
     for (; j < T; j += 2 * kGrp) {
         seg_issue<UNS, NT>(B, A0, j + kGrp, lane, T, zero);
         __builtin_amdgcn_sched_barrier(0);
-        seg_accum<UNS, PL>(A, pre, stage, j, lane, cs, ce, c0, carry, Ps, Pe, hs, he, h1);
+        seg_accum<UNS, HC>(A, pre, stage, j, lane, cs, ce, c0, carry, Ps, Pe, hs, he, h1, h2);
         __builtin_amdgcn_sched_barrier(0);
         seg_issue<UNS, NT>(A, A0, j + 2 * kGrp, lane, T, zero);
         __builtin_amdgcn_sched_barrier(0);
-        seg_accum<UNS, PL>(B, pre, stage, j + kGrp, lane, cs, ce, c0, carry, Ps, Pe, hs, he, h1);
+        seg_accum<UNS, HC>(B, pre, stage, j + kGrp, lane, cs, ce, c0, carry, Ps, Pe, hs, he, h1,
+                           h2);
         __builtin_amdgcn_sched_barrier(0);
     }
     if (ce >= j) // the packet ends exactly at the last row group's end
@@ -1129,8 +1141,8 @@ __device__ __forceinline__ uint16_t seg_tile(uint32_t *pre, u32x4 *stage, int la
         // Header bytes 0..11 from the packet's first two chunks (hs = c0, h1 =
         // c0 + 1); the start chunk cs is one of them.
         const uint32_t s = (uint32_t)(a & 15u);
-        const uint32_t w0 = win_bytes(hs, h1, s, 0), w1 = win_bytes(hs, h1, s, 1),
-                       w2 = win_bytes(hs, h1, s, 2);
+        const uint32_t w0 = win_bytes(hs, h1, h2, s, 0), w1 = win_bytes(hs, h1, h2, s, 1),
+                       w2 = win_bytes(hs, h1, h2, s, 2);
         const PseudoHdr ph = pseudo_hdr(w0 & 0xFFu, (w0 >> 16) & 0xFFu, w0 >> 24,
                                         (w1 >> 16) & 0xFFu);
         if (__ballot(valid && !seg_payload_ok(a, len, ph))) {
@@ -1157,6 +1169,7 @@ __device__ __forceinline__ uint16_t seg_tile(uint32_t *pre, u32x4 *stage, int la
         // options [20, hl), or plus [hl, 20) (src/dst then count twice, as in
         // the reference).  <= 40 bytes, <= 4 chunks, loaded by those lanes.
         const bool corr = ph.v4 && ph.hl != 20u;
+        uint32_t cv = 0;
         if (__ballot(valid && corr)) {
             const int clo = (int)min(ph.hl, 20u), chi = (int)max(ph.hl, 20u);
             const uint64_t ca = (a + (uint32_t)clo) & ~15ull;
@@ -1165,12 +1178,29 @@ __device__ __forceinline__ uint16_t seg_tile(uint32_t *pre, u32x4 *stage, int la
             for (int k = 0; k < 4; ++k)
                 xc[k] = load_chunk<false>(valid && corr && ca + 16ull * k < a + (uint32_t)chi
                                               ? ca + 16ull * k : zero);
-            uint32_t cv = 0;
 #pragma unroll
             for (int k = 0; k < 4; ++k)
                 cv += seg_range(xc[k], (int)(ca - a) + 16 * k, clo, chi);
             if (corr)
                 v = ph.hl < 20u ? v + cv : v - cv;
+        }
+        if constexpr (HDR) {
+            // Fused IPv4 header checksum ip_cksum(ip, hl) (ip4.c:110-115),
+            // 0 for IPv6: V of bytes 0..19 from the staged chunks (each
+            // dword's bytes at their address weight, as wsum of the dword,
+            // byte-swapped per word for an odd start), then minus the bytes
+            // [hl, 20) or plus [20, hl) summed above.  Folded like ip_cksum.
+            const uint32_t w3 = win_bytes(hs, h1, h2, s, 3), w4 = win_bytes(hs, h1, h2, s, 4);
+            const uint32_t sw = odd ? 0x02030001u : 0x03020100u;
+            uint32_t vh = wsum(__builtin_amdgcn_perm(w0, w0, sw), 0u);
+            vh = wsum(__builtin_amdgcn_perm(w1, w1, sw), vh);
+            vh = wsum(__builtin_amdgcn_perm(w2, w2, sw), vh);
+            vh = wsum(__builtin_amdgcn_perm(w3, w3, sw), vh);
+            vh = wsum(__builtin_amdgcn_perm(w4, w4, sw), vh);
+            if (corr)
+                vh = ph.hl < 20u ? vh - cv : vh + cv;
+            rh = !ph.v4 ? (uint16_t)0
+                        : fold_not(odd ? __builtin_amdgcn_alignbit(vh, vh, 24) : vh);
         }
         if (!odd)
             return fold_not(v + ph.special); // exact, wrap included
@@ -1207,6 +1237,7 @@ struct GrpDesc { // one per packet of the tile, in LDS
 struct GrpLds {
     GrpDesc gd[64];
     uint32_t res[64];
+    uint32_t res_h[64]; // fused IPv4 header checksums (HDR)
 };
 
 // Issue-side walk state: quad q, row k within it, and the quad's descriptor
@@ -1261,6 +1292,7 @@ struct GrpAcc {
     uint32_t q, k;
     uint32_t s, len, hl, v4, special;
     uint32_t E, O;
+    uint32_t Eh, Oh; // IP header bytes [0, hl) (HDR)
 };
 
 __device__ __forceinline__ void grp_acc_quad(GrpAcc &S, const GrpLds &L, int lane)
@@ -1273,7 +1305,7 @@ __device__ __forceinline__ void grp_acc_quad(GrpAcc &S, const GrpLds &L, int lan
     S.special = g.special;
 }
 
-template <int UNG, int KIND>
+template <int UNG, int KIND, bool HDR>
 __device__ __forceinline__ void grp_accum(const GrpRows<UNG> &R, GrpAcc &S, GrpLds &L, int lane,
                                           uint32_t Rq)
 {
@@ -1284,10 +1316,9 @@ __device__ __forceinline__ void grp_accum(const GrpRows<UNG> &R, GrpAcc &S, GrpL
             const uint32_t c = 16u * S.k + gl;
             const uint32_t span = grp_span<KIND>(S.len);
             const uint32_t nch = span ? (S.s + span + 15u) >> 4 : 0u;
-            uint32_t eh = 0, oh = 0;
-            accum_strided<KIND, false, false>(R.d[u], 16 * (int)c - (int)S.s,
-                                              KIND == WC_KIND_PAYLOAD ? (int)S.hl : 0,
-                                              (int)S.len, c < nch, S.v4, S.E, S.O, eh, oh);
+            accum_strided<KIND, false, HDR>(R.d[u], 16 * (int)c - (int)S.s,
+                                            KIND == WC_KIND_PAYLOAD ? (int)S.hl : 0,
+                                            (int)S.len, c < nch, S.v4, S.E, S.O, S.Eh, S.Oh);
             if (++S.k == Rq) {
                 // Quad done: exact reference accumulator of each packet
                 // (in_cksum.c:140-167 / 107-120, mod 2^32), row scan to lane 15.
@@ -1298,6 +1329,17 @@ __device__ __forceinline__ void grp_accum(const GrpRows<UNG> &R, GrpAcc &S, GrpL
                 x += dpp0<kDppRowShr + 8, 0xF>(x);
                 if (gl == 15u)
                     L.res[4u * S.q + ((uint32_t)lane >> 4)] = fold_not(x);
+                if constexpr (HDR) {
+                    // ip_cksum(ip, hl) of IPv4 packets (ip4.c:110-115)
+                    uint32_t h = combine(S.Eh, S.Oh, S.s & 1u);
+                    h += dpp0<kDppRowShr + 1, 0xF>(h);
+                    h += dpp0<kDppRowShr + 2, 0xF>(h);
+                    h += dpp0<kDppRowShr + 4, 0xF>(h);
+                    h += dpp0<kDppRowShr + 8, 0xF>(h);
+                    if (gl == 15u)
+                        L.res_h[4u * S.q + ((uint32_t)lane >> 4)] = S.v4 ? fold_not(h) : 0u;
+                    S.Eh = S.Oh = 0u;
+                }
                 S.E = S.O = 0u;
                 S.k = 0;
                 ++S.q;
@@ -1310,9 +1352,10 @@ __device__ __forceinline__ void grp_accum(const GrpRows<UNG> &R, GrpAcc &S, GrpL
 // One uniform tile.  Returns this lane's packet's checksum, or done = false
 // (payload_cksum with a header longer than its packet: the caller takes the
 // flat path).
-template <int UNG, int KIND, bool NT>
+template <int UNG, int KIND, bool NT, bool HDR>
 __device__ __forceinline__ uint16_t grp_tile(GrpLds &L, int lane, uint64_t a, uint32_t len,
-                                             bool valid, uint32_t Rq, uint64_t zero, bool &done)
+                                             bool valid, uint32_t Rq, uint64_t zero, bool &done,
+                                             uint16_t &rh)
 {
     // payload_cksum's header bytes: loaded first, waited for only after the
     // first row group is issued (the addresses need no header).
@@ -1345,14 +1388,16 @@ __device__ __forceinline__ uint16_t grp_tile(GrpLds &L, int lane, uint64_t a, ui
     for (uint32_t j = 0; j < rows; j += 2u * UNG) {
         grp_issue<UNG, KIND, NT>(B, I, L, lane, Rq, zero);
         __builtin_amdgcn_sched_barrier(0);
-        grp_accum<UNG, KIND>(A, S, L, lane, Rq);
+        grp_accum<UNG, KIND, HDR>(A, S, L, lane, Rq);
         __builtin_amdgcn_sched_barrier(0);
         grp_issue<UNG, KIND, NT>(A, I, L, lane, Rq, zero);
         __builtin_amdgcn_sched_barrier(0);
-        grp_accum<UNG, KIND>(B, S, L, lane, Rq);
+        grp_accum<UNG, KIND, HDR>(B, S, L, lane, Rq);
         __builtin_amdgcn_sched_barrier(0);
     }
     wave_order();
+    if constexpr (HDR)
+        rh = (uint16_t)L.res_h[lane];
     return (uint16_t)L.res[lane];
 }
 
@@ -1385,13 +1430,14 @@ __device__ __forceinline__ bool seg_dense(int lane, uint64_t a, uint32_t len, bo
 // slen bytes) -- packed packets at any alignment are one dense byte range,
 // which the seg path streams better than the group kernel masks its
 // boundary chunks; offsets and lengths are computed, not loaded.
-template <int UN, int UNS, int UNG, int KIND, bool NT, bool STR>
+template <int UN, int UNS, int UNG, int KIND, bool NT, bool STR, bool HDR = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UNS >= 8 ? 2 : 4)))
 k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
             const uint16_t *__restrict__ lens, uint64_t n, uint16_t *__restrict__ out,
             unsigned long long *__restrict__ bad, int grp_thr, int variant, uint64_t stride,
-            uint32_t slen)
+            uint32_t slen, uint16_t *__restrict__ out_hdr)
 {
+    static_assert(!HDR || KIND == WC_KIND_PAYLOAD, "header checksum rides on payload");
     (void)variant; // WC_VARIANT: A/B experiments
     union TileLds {
         FlatLds<UN> flat;
@@ -1450,11 +1496,12 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
         const uint32_t thr = dense ? (uint32_t)(grp_thr & 0xFF) : (uint32_t)(grp_thr >> 8);
         const bool grouped = Rq != 0 && (uint64_t)fill * 64u >= (uint64_t)thr * 1024u * Rq;
         bool done = false;
+        uint16_t rh = 0;
         if (grouped)
-            r = grp_tile<UNG, KIND, NT>(L.grp, lane, a, len, valid, Rq, zero, done);
+            r = grp_tile<UNG, KIND, NT, HDR>(L.grp, lane, a, len, valid, Rq, zero, done, rh);
         else if (dense)
-            r = seg_tile<UNS, KIND, NT>(L.seg.pre, L.seg.stage, lane, a, len, valid, A0, T, zero,
-                                        done);
+            r = seg_tile<UNS, KIND, NT, HDR>(L.seg.pre, L.seg.stage, lane, a, len, valid, A0, T,
+                                             zero, done, rh);
         if (!done) {
             PseudoHdr ph{0u, 1u, 0u};
             if constexpr (KIND == WC_KIND_PAYLOAD)
@@ -1463,7 +1510,12 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
             wave_order();
             r = fold_not(flat_tile_sum<UN, KIND, NT, false, true>(L.flat, nullptr, lane, a, len,
                                                                   valid, ph, [] {}));
+            if constexpr (HDR)
+                rh = valid && ph.v4 ? lane_hdr_cksum<NT>(a, ph.hl, nullptr) : (uint16_t)0;
         }
+        if constexpr (HDR)
+            if (valid)
+                out_hdr[p] = rh;
         if (valid && out)
             out[p] = r;
         nbad += valid && r != 0;
@@ -1585,11 +1637,18 @@ static hipError_t launch_flat_un(const LaunchArgs &a, hipStream_t st)
                            dim3(256), 0, st, b, a.offs, a.lens, a.n, a.out, bad, a.out_hdr);
         return hipGetLastError();
     }
+    if (a.seg_rows && a.out_hdr && a.kind == WC_KIND_PAYLOAD && a.offs) {
+        // fused IPv4 header + payload_cksum pass, default row-group sizes
+        hipLaunchKernelGGL((k_cksum_seg<UN, 4, 4, WC_KIND_PAYLOAD, true, false, true>),
+                           dim3(grid), dim3(256), 0, st, b, a.offs, a.lens, a.n, a.out, bad,
+                           a.grp_thr, a.variant, a.stride, a.len, a.out_hdr);
+        return hipGetLastError();
+    }
     if (a.seg_rows && !a.out_hdr) {
 #define WC_SEG_K(K, S)                                                         \
     hipLaunchKernelGGL((k_cksum_seg<UN, US, UG, K, true, S>), dim3(grid), dim3(256), 0, st, \
                        b, a.offs, a.lens, a.n, a.out, bad, a.grp_thr, a.variant, a.stride, \
-                       a.len)
+                       a.len, nullptr)
 #define WC_SEG(US_, UG_)                                                       \
     {                                                                          \
         constexpr int US = US_, UG = UG_;                                      \
