@@ -312,6 +312,26 @@ def main():
     parity["checked_packets"] = wdist.sum_over_ranks(parity["checked_packets"], coll_dev)
     parity["mismatches"] = wdist.sum_over_ranks(parity["mismatches"], coll_dev)
 
+    # after the timed region the ranks exchange their 2-byte
+    # results (RCCL all-gather over xGMI; host tensors for the gloo
+    # rehearsal), so every rank holds the whole job's results in packet order.
+    gather = None
+    if world > 1 and out.numel() == n:
+        src = out.view(torch.int16)
+        if coll_dev.type != "cuda":
+            src = src.cpu()
+        wdist.barrier(dev)
+        t_g = time.perf_counter()
+        allr = wdist.gather_results(src, world * n)
+        if coll_dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+        g_ms = (time.perf_counter() - t_g) * 1e3
+        lo, hi = wdist.shard_range(world * n, rank, world)
+        bad = int(not torch.equal(allr[lo:hi].cpu(), out.view(torch.int16).cpu()))
+        gather = {"collective": "all_gather", "bytes_per_rank": 2 * n,
+                  "ms": round(wdist.max_over_ranks(g_ms, coll_dev), 3),
+                  "ranks_mismatched": wdist.sum_over_ranks(bad, coll_dev)}
+
     traffic = None
     try:
         tf = json.loads(Path(args.traffic_file).read_text())
@@ -356,6 +376,8 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
         }
+        if gather is not None:
+            line["results_allgather"] = gather
         print(json.dumps(line), flush=True)
     if world > 1:
         import torch.distributed as dist

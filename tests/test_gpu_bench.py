@@ -52,6 +52,8 @@ def test_bench_two_ranks_rehearsal(gpu):
     assert line["n_gpus"] == 2 and line["scaling"] == "weak"
     assert line["cpu_baseline"] is None
     assert line["parity"] == {"checked_packets": 2 * 65536, "mismatches": 0}
+    assert line["results_allgather"]["ranks_mismatched"] == 0
+    assert line["results_allgather"]["bytes_per_rank"] == 2 * 65536
 
 
 @pytest.mark.parametrize("args", [["--config", "c4", "--packets", "200000"],
