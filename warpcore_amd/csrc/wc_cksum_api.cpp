@@ -276,8 +276,9 @@ Plan plan_ragged(const Device &D, uint64_t n, int kind, bool zero_copy = false,
     (void)D;
     Plan p;
     p.full = false;
-    const bool small = (zero_copy && n <= kZcGroupMax) ||
-                       n < (uint64_t)env_int("WC_FLAT_MIN", kFlatMinDefault);
+    const bool small =
+        (zero_copy && n <= (uint64_t)env_int("WC_ZC_GROUP_MAX", (int)kZcGroupMax)) ||
+        n < (uint64_t)env_int("WC_FLAT_MIN", kFlatMinDefault);
     if (small && !hdr) {
         p.shape = {64, 2, 1};
         parse_shape(getenv("WC_RAGGED_SHAPE"), &p.shape);
@@ -288,7 +289,7 @@ Plan plan_ragged(const Device &D, uint64_t n, int kind, bool zero_copy = false,
     p.shape = {0, 1, env_int("WC_FLAT_UN", 2)};
     p.grid = 0;
     const int seg = env_int("WC_SEG", 1);
-    if (!zero_copy && env_int("WC_DIAG_NOLOAD", 0) == 0 && seg != 0 &&
+    if ((!zero_copy || env_int("WC_ZC_SEG", 0)) && env_int("WC_DIAG_NOLOAD", 0) == 0 && seg != 0 &&
         (!hdr || kind == WC_CKSUM_PAYLOAD))
         p.seg_rows = env_int("WC_SEG_ROWS", 4);
     return p;
