@@ -62,20 +62,27 @@ __device__ __forceinline__ uint32_t pick_byte(const u32x4 &d, int pos)
     return (pick_dword(d, pos >> 2) >> (8 * (pos & 3))) & 0xFFu;
 }
 
-// Logical block of this workgroup, XCD-contiguous: workgroups are placed on
-// the 8 XCDs round-robin (blockIdx.x % 8), so XCD x gets logical blocks
-// [x q + min(x, r), + q + (x < r)) -- one contiguous eighth of the batch per
-// XCD instead of interleaved 1/8-strips (q = grid / 8, r = grid % 8; a
-// bijection for any grid).  Measured: 9000-B packets 86.8 -> 92.6 % of HBM
-// peak, netmap-slot batches +1.5..2.3 points, C2 +0.4, nothing slower
-// (profiles/ab_r01_xcd_remap.log).  WC_VARIANT bit 8 turns it off (A/B).
+// Logical block of this workgroup, XCD-contiguous within super-blocks of
+// 4096 workgroups: workgroups are placed on the 8 XCDs round-robin
+// (blockIdx.x % 8), so inside each super-block XCD x gets logical blocks
+// [x q + min(x, r), + q + (x < r)) -- one contiguous eighth of the
+// super-block per XCD instead of interleaved 1/8-strips (q = m / 8, r = m % 8
+// for a super-block of m workgroups; a bijection for any grid).  Bounding the
+// span keeps the 8 XCDs' streams within a few hundred MB of each other:
+// remapping the whole grid left them gigabytes apart and cost up to 8 points
+// on large batches (address-translation reach).  Measured vs no remap and vs
+// a whole-grid remap: profiles/ab_r01_xcd_remap.log.  WC_VARIANT bit 8 turns
+// it off, bits 8..15 = k set the span to 2^k (k >= 31: whole grid) (A/B).
 __device__ __forceinline__ uint64_t xcd_block(int variant)
 {
     const uint32_t b = blockIdx.x, nb = gridDim.x;
     if (variant & 8)
         return b;
-    const uint32_t x = b & 7u, q = nb >> 3, r = nb & 7u;
-    return (uint64_t)(x * q + min(x, r) + (b >> 3));
+    const uint32_t k = ((uint32_t)variant >> 8) & 0xFFu;
+    const uint32_t span = k == 0 ? 4096u : k >= 31 ? nb : (1u << k);
+    const uint32_t base = b / span * span, m = min(span, nb - base), l = b - base;
+    const uint32_t x = l & 7u, q = m >> 3, r = m & 7u;
+    return (uint64_t)(base + x * q + min(x, r) + (l >> 3));
 }
 
 // Global (addrspace 1) pointer: lets hipcc emit global_load_dwordx4 rather
