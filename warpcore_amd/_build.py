@@ -14,6 +14,7 @@ import os
 import platform
 import subprocess
 import sys
+import tempfile
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
@@ -23,8 +24,10 @@ INCLUDE = ROOT / "include"
 LIB = PKG / "libwccksum.so"
 ORACLE_DIR = ROOT / "oracle"
 
-HIP_SOURCES = [CSRC / "wc_cksum_kernels.hip", CSRC / "wc_cksum_api.cpp"]
-HIP_DEPS = HIP_SOURCES + [CSRC / "wc_cksum_kernels.h", INCLUDE / "warpcore_gpu" / "wc_cksum.h"]
+HIP_SOURCES = [CSRC / "wc_k_strided.hip", CSRC / "wc_k_seg.hip", CSRC / "wc_k_flat.hip",
+               CSRC / "wc_k_synth.hip", CSRC / "wc_cksum_api.cpp"]
+HIP_DEPS = HIP_SOURCES + [CSRC / "wc_cksum_kernels.h", CSRC / "wc_device.h", CSRC / "wc_flat.h",
+                          INCLUDE / "warpcore_gpu" / "wc_cksum.h"]
 ORACLE_SOURCES = [ORACLE_DIR / "wc_oracle.c", ORACLE_DIR / "wc_oracle.h"]
 
 
@@ -43,18 +46,29 @@ def _stale(target: Path, deps) -> bool:
 
 
 def build_lib(force: bool = False, verbose: bool = False) -> Path:
-    """Compile libwccksum.so for gfx950 (cross-compiles without a GPU)."""
+    """Compile libwccksum.so for gfx950 (cross-compiles without a GPU): every
+    translation unit in parallel into a scratch directory, then one link."""
     if not force and not _stale(LIB, HIP_DEPS):
         return LIB
-    tmp = LIB.with_suffix(".so.tmp")
-    cmd = [
-        _hipcc(), "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-        "-Wall", f"-I{INCLUDE}", f"-I{CSRC}", "-o", str(tmp),
-        *[str(s) for s in HIP_SOURCES],
-    ]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.run(cmd, check=True)
+    flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall",
+             f"-I{INCLUDE}", f"-I{CSRC}"]
+    with tempfile.TemporaryDirectory(prefix="wccksum-") as tmpdir:
+        objs, procs = [], []
+        for src in HIP_SOURCES:
+            obj = Path(tmpdir) / (src.stem + ".o")
+            cmd = [_hipcc(), *flags, "-c", str(src), "-o", str(obj)]
+            if verbose:
+                print(" ".join(cmd), file=sys.stderr)
+            procs.append((cmd, subprocess.Popen(cmd)))
+            objs.append(str(obj))
+        failed = [cmd for cmd, p in procs if p.wait() != 0]
+        if failed:
+            raise subprocess.CalledProcessError(1, failed[0])
+        tmp = LIB.with_suffix(".so.tmp")
+        cmd = [_hipcc(), "--offload-arch=gfx950", "-fPIC", "-shared", "-o", str(tmp), *objs]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
     os.replace(tmp, LIB)
     return LIB
 

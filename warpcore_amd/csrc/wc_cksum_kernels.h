@@ -1,5 +1,5 @@
 // wc_cksum_kernels.h -- internal interface between the C-ABI layer
-// (wc_cksum_api.cpp) and the gfx950 kernels (wc_cksum_kernels.hip).
+// (wc_cksum_api.cpp) and the gfx950 kernels (wc_k_*.hip, wc_device.h).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -87,6 +87,8 @@ hipError_t launch_cksum(const LaunchArgs &a, const Shape &sh, int grid,
 // tiles; the rest take its flat path), else the chunk-balanced flat kernel
 // (rows = 64-chunk rows per ping-pong group: 1, 2 or 4).
 hipError_t launch_flat(const LaunchArgs &a, int rows, hipStream_t st);
+// The standalone flat kernel (wc_k_flat.hip), behind launch_flat.
+hipError_t launch_flat_kernel(const LaunchArgs &a, int rows, hipStream_t st);
 hipError_t launch_synth(void *buf, uint64_t nbytes, uint64_t seed, int grid,
                         hipStream_t st);
 

@@ -1,0 +1,281 @@
+// wc_flat.h -- device code of the chunk-balanced "flat" tile path, shared by
+// k_cksum_flat (wc_k_flat.hip) and the flat fallback of k_cksum_seg
+// (wc_k_seg.hip).
+#pragma once
+
+#include "wc_device.h"
+
+namespace wc {
+namespace {
+
+// ---------------------------------------------------------------------------
+// Ragged batches: chunk-balanced "flat" kernel.
+//
+// A wave owns a tile of 64 consecutive packets (lane l holds packet l's
+// metadata, loaded coalesced).  The tile's 16-byte chunks are numbered
+// 0..T-1 in packet order (wave prefix sum of the per-packet chunk counts) and
+// dealt to the lanes one 64-chunk ROW at a time, so every lane streams a chunk
+// whatever the length mix (Zipf, jumbo frames, empty packets).  Per row:
+//   * owner lookup: each packet whose run of chunks starts inside the row
+//     marks that slot in LDS (tagged with the row number, so nothing needs
+//     clearing); a ballot of the marks gives the run starts, and
+//     rank(owner) = rank(first run) + mbcnt(starts at or below the lane);
+//   * the owner's descriptor (chunk base, start phase, length, header info)
+//     comes from the tile's LDS table, indexed by the rank of the packet
+//     among the tile's non-empty packets;
+//   * byte weights come from the LDS tables above;
+//   * the lanes' exact partial sums go through a DPP inclusive prefix sum and
+//     each packet lane adds P[last slot] - P[first slot - 1] of its run to a
+//     register accumulator -- no atomics, no same-address LDS traffic.
+// Row groups (UN interleaved rows, each load fully coalesced) are
+// ping-ponged, and the next tile's metadata (and, for payload_cksum, its
+// header bytes) is prefetched while the current tile streams.
+
+struct FlatDesc {          // 16 bytes per non-empty packet of the tile, in LDS
+    uint32_t vb_lo, vb_hi; // chunk q of the packet sits at vb + 16 q
+    uint32_t rel;          // packet start in the tile's slot-byte space
+    uint32_t info;         // len | hl << 16 | v4 << 24
+};
+
+template <int UN>
+struct FlatRows {
+    u32x4 d[UN];
+    uint32_t own[UN];
+};
+
+template <int UN>
+struct FlatLds {
+    FlatDesc desc[64];
+    uint32_t mark[UN][64]; // run-start tags, one array per row of a group
+    uint32_t pre[64 * UN]; // inclusive prefix sums of the group's chunk sums
+};
+
+// Intra-wave LDS hand-offs need no fence: one wave's LDS instructions execute
+// in issue order.  wave_barrier only stops hipcc moving LDS accesses across.
+__device__ __forceinline__ void wave_order()
+{
+    __builtin_amdgcn_wave_barrier();
+}
+
+// Owner lookup + loads for the UN rows of a group starting at slot g0.
+template <int UN, bool NT, bool NOLOAD = false>
+__device__ __forceinline__ void flat_issue(FlatRows<UN> &R, FlatLds<UN> &L,
+                                           uint32_t g0, int lane, uint32_t cp,
+                                           uint32_t ce, uint32_t rank,
+                                           uint32_t last_rank, uint32_t total)
+{
+    uint32_t first[UN];
+#pragma unroll
+    for (int u = 0; u < UN; ++u) {
+        const uint32_t row0 = g0 + 64u * u;
+        // Packet lane: its run inside this row is [lo, hi); a run that starts
+        // inside the row (not at its first slot) marks its first slot with
+        // the row's tag.
+        const uint32_t lo = max(cp, row0), hi = min(ce, row0 + 64u);
+        const bool part = lo < hi;
+        if (part && lo > row0)
+            L.mark[u][lo - row0] = row0 >> 6;
+        // Rank of the packet covering the row's first slot; a row past the
+        // tile's end has none and takes the last packet (its loads are
+        // clamped to the tile's last chunk, which that packet owns).
+        const uint64_t firstm = __ballot(part && lo == row0);
+        first[u] = firstm ? __builtin_amdgcn_readlane(rank, (int)__builtin_ctzll(firstm))
+                          : last_rank;
+    }
+    wave_order();
+#pragma unroll
+    for (int u = 0; u < UN; ++u) {
+        const uint32_t row0 = g0 + 64u * u;
+        const bool st = L.mark[u][lane] == (row0 >> 6);
+        const uint32_t own = min(first[u] + mbcnt64(__ballot(st)) + (st ? 1u : 0u), last_rank);
+        R.own[u] = own;
+        const uint64_t vb = *reinterpret_cast<const uint64_t *>(&L.desc[own]);
+        // Unconditional load (slots past the tile's end re-read its last
+        // chunk and are zeroed in flat_accum): a straight-line issue stream
+        // lets hipcc wait for exactly the older row group.
+        const uint32_t q = min(row0 + (uint32_t)lane, total - 1u);
+        if constexpr (NOLOAD) // diagnostic build: same stream, no HBM traffic
+            R.d[u] = u32x4{(uint32_t)vb, q, (uint32_t)(vb >> 32), q ^ 0x5a5a5a5au};
+        else
+            R.d[u] = load_chunk<NT>(vb + 16ull * q);
+    }
+}
+
+template <int UN, int KIND, bool ARITH = false>
+__device__ __forceinline__ void flat_accum(const FlatRows<UN> &R, FlatLds<UN> &L,
+                                           const WeightLut *M, uint32_t g0,
+                                           int lane, uint32_t cp, uint32_t ce,
+                                           uint32_t total, uint32_t &acc)
+{
+    uint32_t P[UN];
+#pragma unroll
+    for (int u = 0; u < UN; ++u) {
+        const uint32_t q = g0 + 64u * u + (uint32_t)lane;
+        const FlatDesc &g = L.desc[R.own[u]];
+        const uint32_t rel = g.rel, info = g.info;
+        uint32_t E = 0, O = 0;
+        if constexpr (ARITH)
+            accum_arith<KIND>(R.d[u], (int)(16u * q - rel), (int)((info >> 16) & 0xFFu),
+                              (int)(info & 0xFFFFu), (info >> 24) & 1u, E, O);
+        else
+            accum_masked<KIND>(R.d[u], (int)(16u * q - rel), (int)((info >> 16) & 0xFFu),
+                               (int)(info & 0xFFFFu), (info >> 24) & 1u, *M, E, O);
+        P[u] = q < total ? combine(E, O, rel & 1u) : 0u;
+    }
+    // Inclusive prefix sums of the UN rows, step-interleaved so each row's DPP
+    // step fills the others' hazard slots; then the rows are chained.
+#define WC_SCAN_STEP(CTRL, ROWS)                                               \
+    _Pragma("unroll") for (int u = 0; u < UN; ++u) P[u] += dpp0<CTRL, ROWS>(P[u]);
+    WC_SCAN_STEP(kDppRowShr + 1, 0xF)
+    WC_SCAN_STEP(kDppRowShr + 2, 0xF)
+    WC_SCAN_STEP(kDppRowShr + 4, 0xF)
+    WC_SCAN_STEP(kDppRowShr + 8, 0xF)
+    WC_SCAN_STEP(kDppRowBcast15, 0xA)
+    WC_SCAN_STEP(kDppRowBcast31, 0xC)
+#undef WC_SCAN_STEP
+    uint32_t carry = 0;
+#pragma unroll
+    for (int u = 0; u < UN; ++u) {
+        const uint32_t tot = __builtin_amdgcn_readlane(P[u], 63);
+        L.pre[64 * u + lane] = P[u] + carry;
+        carry += tot;
+    }
+    wave_order();
+    // Packet lane: Σ over its run [rlo, rhi) of the group.
+    constexpr uint32_t kGrp = 64u * UN;
+    const uint32_t rlo = max(cp, g0), rhi = min(ce, g0 + kGrp);
+    const uint32_t e_last = min(rhi - g0 - 1u, kGrp - 1u);
+    const uint32_t e_before = rlo > g0 ? min(rlo - g0 - 1u, kGrp - 1u) : 0u;
+    const uint32_t pe = L.pre[e_last];
+    const uint32_t pb = L.pre[e_before];
+    if (rlo < rhi)
+        acc += pe - (rlo > g0 ? pb : 0u);
+    wave_order(); // pre is rewritten by the next group
+}
+
+// payload_cksum's header bytes, prefetched a tile ahead: ONE 16-byte load at
+// the 4-byte boundary at or below the packet start (a scattered load moves a
+// whole cache line per lane, so one load instead of several byte loads).  It
+// covers packet bytes 0..12, inside the header the reference reads anyway
+// (in_cksum.c:142-160), so it never touches a page the reference would not.
+// The bytes are picked out at their use (hdr_h0 / hdr_h1), not at the load:
+// extracting them right away made hipcc wait for the load -- and for every
+// stream load issued before it -- at the prefetch.
+typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+
+struct HdrRaw {
+    u32x4 d;
+};
+
+__device__ __forceinline__ HdrRaw load_hdr(uint64_t a)
+{
+    return HdrRaw{*(const u32x4a4 __attribute__((address_space(1))) *)(uintptr_t)(a & ~3ull)};
+}
+
+// b0 | b2 << 8 | b3 << 16 | b6 << 24 of the packet at a.
+__device__ __forceinline__ uint32_t hdr_h0(const HdrRaw &h, uint64_t a)
+{
+    const uint32_t sh = 8u * (uint32_t)(a & 3u);
+    const uint32_t w0 = __builtin_amdgcn_alignbit(h.d.y, h.d.x, sh); // bytes 0..3
+    const uint32_t w1 = __builtin_amdgcn_alignbit(h.d.z, h.d.y, sh); // bytes 4..7
+    return __builtin_amdgcn_perm(w1, w0, 0x06030200u);
+}
+
+// b4 | b5 << 8 | b9 << 16 of the packet at a.
+__device__ __forceinline__ uint32_t hdr_h1(const HdrRaw &h, uint64_t a)
+{
+    const uint32_t sh = 8u * (uint32_t)(a & 3u);
+    const uint32_t w1 = __builtin_amdgcn_alignbit(h.d.z, h.d.y, sh); // bytes 4..7
+    const uint32_t w2 = __builtin_amdgcn_alignbit(h.d.w, h.d.z, sh); // bytes 8..11
+    return __builtin_amdgcn_perm(w2, w1, 0x0C050100u);
+}
+
+__device__ __forceinline__ PseudoHdr hdr_pseudo(const HdrRaw &h, uint64_t a)
+{
+    const uint32_t h0 = hdr_h0(h, a);
+    return pseudo_hdr(h0 & 0xFFu, (h0 >> 8) & 0xFFu, (h0 >> 16) & 0xFFu, h0 >> 24);
+}
+
+// Fused IPv4 header checksum for the flat kernel: the packet's own lane sums
+// its header [0, hl) (at most 5 chunks) -- ip_cksum(ip, hl), ip4.c:110-115.
+template <bool NT>
+__device__ __forceinline__ uint16_t lane_hdr_cksum(uint64_t a, uint32_t hl,
+                                                   const WeightLut *M)
+{
+    const uint32_t s = (uint32_t)(a & 15u);
+    const uint64_t c0 = a & ~15ull;
+    const uint32_t nh = (s + hl + 15u) >> 4;
+    uint32_t E = 0, O = 0;
+    for (uint32_t k = 0; k < nh; ++k) {
+        const u32x4 d = load_chunk<false>(c0 + 16ull * k);
+        const int co = (int)(16u * k) - (int)s;
+        if (M) // the flat kernel's LDS tables, or arithmetic masks
+            accum_masked<WC_KIND_IP>(d, co, 0, (int)hl, 0u, *M, E, O);
+        else
+            accum_arith<WC_KIND_IP>(d, co, 0, (int)hl, 0u, E, O);
+    }
+    return fold_not(combine(E, O, s & 1u));
+}
+
+// One 64-packet tile of the flat kernel: returns this lane's packet's exact
+// reference accumulator (in_cksum.c:140-167 / 107-120, mod 2^32) -- the
+// caller folds it.  `after_first_issue` runs once the tile's first row group
+// is in flight (the caller's next-tile prefetch goes there).
+template <int UN, int KIND, bool NT, bool NOLOAD, bool ARITH, class F>
+__device__ __forceinline__ uint32_t flat_tile_sum(FlatLds<UN> &L, const WeightLut *lut,
+                                                  int lane, uint64_t a, uint32_t len,
+                                                  bool valid, const PseudoHdr &ph,
+                                                  F &&after_first_issue)
+{
+    const uint32_t s = (uint32_t)(a & 15u);
+    const uint32_t span = KIND == WC_KIND_PAYLOAD ? max(len, 20u) : len;
+    const uint32_t nch = valid ? (s + span + 15u) >> 4 : 0u;
+
+    // Chunk-slot range [cp, ce) of this lane's packet within the tile;
+    // rank among the tile's non-empty packets.
+    const uint32_t ce = wave_incl_sum(nch);
+    const uint32_t cp = ce - nch;
+    const uint32_t total = lane_u32(ce, 63);
+    const uint64_t nonempty = __ballot(nch != 0);
+    const uint32_t rank = mbcnt64(nonempty);
+    const uint32_t last_rank = nonempty ? (uint32_t)__builtin_popcountll(nonempty) - 1u : 0u;
+    const uint64_t vb = (a & ~15ull) - 16ull * cp;
+    if (nch != 0)
+        L.desc[rank] = FlatDesc{(uint32_t)vb, (uint32_t)(vb >> 32), s + 16u * cp,
+                                len | (ph.hl << 16) | (ph.v4 << 24)};
+    // Row marks carry the row's number within the tile; reset them to a
+    // tag no row has so the previous tile's marks can't match.
+#pragma unroll
+    for (int u = 0; u < UN; ++u)
+        L.mark[u][lane] = 0xFFFFFFFFu;
+    wave_order();
+
+    uint32_t acc = ph.special;
+    constexpr uint32_t kGrp = 64u * UN;
+    FlatRows<UN> A, B;
+    if (total != 0)
+        flat_issue<UN, NT, NOLOAD>(A, L, 0, lane, cp, ce, rank, last_rank, total);
+    after_first_issue();
+    if (total != 0) {
+        // Ping-pong row groups A / B (no register copies): group g+1's
+        // loads are in flight while group g is summed.  No exit between
+        // the halves: a half past the tile's end sums zeros, and keeping
+        // each load's use in the next half stops hipcc sinking the load
+        // next to it; sched_barrier keeps each issue ahead of the other
+        // group's sum.
+        for (uint32_t j = 0; j < total; j += 2 * kGrp) {
+            flat_issue<UN, NT, NOLOAD>(B, L, j + kGrp, lane, cp, ce, rank, last_rank, total);
+            __builtin_amdgcn_sched_barrier(0);
+            flat_accum<UN, KIND, ARITH>(A, L, lut, j, lane, cp, ce, total, acc);
+            __builtin_amdgcn_sched_barrier(0);
+            flat_issue<UN, NT, NOLOAD>(A, L, j + 2 * kGrp, lane, cp, ce, rank, last_rank, total);
+            __builtin_amdgcn_sched_barrier(0);
+            flat_accum<UN, KIND, ARITH>(B, L, lut, j + kGrp, lane, cp, ce, total, acc);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+    return acc;
+}
+
+} // namespace
+} // namespace wc

@@ -1,0 +1,211 @@
+// wc_k_strided.hip -- strided batches on gfx950: the group-per-packet kernel
+// k_cksum and its launch table.
+#include "wc_device.h"
+
+namespace wc {
+
+// ---------------------------------------------------------------------------
+// Strided batches: group-per-packet kernel.
+//   G     lanes per packet (power of two, 4..64)
+//   CPL   16-byte chunk loads per lane per pass (a pass covers G*CPL chunks)
+//   U     packets per group per iteration (more bytes in flight for small
+//         packets)
+//   KIND  WC_KIND_IP / WC_KIND_PAYLOAD
+//   FULL  every packet starts 16-byte aligned and len % 16 == 0 (IP only):
+//         no masks, no tables
+//   NT    nontemporal loads
+//   HDR   (payload only) also store ip_cksum(ip, ip4_hl) of each IPv4 packet
+//         into out_hdr (0 for IPv6, which has no header checksum)
+//   RAGGED packet i is [base + offs[i], + lens[i]) instead: the small-batch
+//         ragged variant (a few packets per wave, so a batch far smaller than
+//         the GPU still puts every packet's loads in flight at once)
+// Packet i is [base + i*stride, + len).  The grid is one-shot by default
+// (each wave does one iteration); a capped grid strides.  waves_per_eu(3)
+// caps the kernel at 168 VGPRs: payload (16,6,4) otherwise takes 170, which
+// leaves 2 waves per SIMD and cost 10 % of HBM throughput (80 -> 88 % of peak,
+// profiles/ab_r01_c2_payload_waves.log).
+template <int G, int CPL, int U, int KIND, bool FULL, bool NT, bool HDR, bool RAGGED>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
+k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
+        const uint64_t *__restrict__ offs, const uint16_t *__restrict__ lens,
+        uint64_t n, uint16_t *__restrict__ out, unsigned long long *__restrict__ bad,
+        uint16_t *__restrict__ out_hdr, int variant)
+{
+    static_assert(!(RAGGED && (FULL || HDR)), "ragged group variant: masked, no header");
+    static_assert(!HDR || KIND == WC_KIND_PAYLOAD, "header checksum rides on payload");
+    static_assert(G >= 4 && G <= 64 && (G & (G - 1)) == 0, "group width");
+    static_assert(!(FULL && KIND == WC_KIND_PAYLOAD), "payload needs masks");
+    constexpr int GPW = 64 / G;
+    constexpr uint64_t PPW = (uint64_t)GPW * U;
+    constexpr int PASS = G * CPL;
+
+    const int lane = threadIdx.x & 63;
+    const int gl = lane & (G - 1);
+    const int grp = lane / G;
+    const int lead = lane & ~(G - 1);
+    const uint64_t wave = xcd_block(variant) * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    uint32_t nbad = 0;
+    const uint64_t zero = (uint64_t)(uintptr_t)&kZeroChunk;
+
+    for (uint64_t p0 = wave * PPW; p0 < n; p0 += nwaves * PPW) {
+        uint64_t c0[U];
+        uint32_t nch[U], plen[U];
+        int s[U];
+        bool valid[U];
+        u32x4 d[U][CPL];
+
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = p0 + (uint64_t)u * GPW + grp;
+            valid[u] = i < n;
+            const uint64_t ii = valid[u] ? i : p0;
+            uint64_t a;
+            if constexpr (RAGGED) {
+                a = (uint64_t)base + offs[ii];
+                plen[u] = lens[ii];
+            } else {
+                a = (uint64_t)base + ii * stride;
+                plen[u] = len;
+            }
+            // payload_cksum reads the IPv4 header fields up to byte 19 even
+            // for a shorter len (in_cksum.c:149-151), so cover them too.
+            const uint32_t span = KIND == WC_KIND_PAYLOAD ? max(plen[u], 20u) : plen[u];
+            s[u] = (int)(a & 15u);
+            c0[u] = a & ~15ull;
+            nch[u] = valid[u] ? (uint32_t)((a + span + 15u - c0[u]) >> 4) : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                const uint32_t k = (uint32_t)(gl + c * G);
+                // Unconditional load (no branch per chunk): dead slots read a
+                // zero chunk.
+                d[u][c] = load_chunk<NT>(k < nch[u] ? c0[u] + 16ull * k : zero);
+            }
+
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            PseudoHdr ph{0u, 1u, 0u};
+            if constexpr (KIND == WC_KIND_PAYLOAD) {
+                // Header bytes 0, 2, 3, 6 sit in the group's chunks 0/1, i.e.
+                // in d[u][0] of group lanes 0 and 1.
+                const int su = s[u];
+                const uint32_t b0 = __shfl(pick_byte(d[u][0], su), lead + (su >> 4), 64);
+                const uint32_t b2 = __shfl(pick_byte(d[u][0], (su + 2) & 15),
+                                           lead + ((su + 2) >> 4), 64);
+                const uint32_t b3 = __shfl(pick_byte(d[u][0], (su + 3) & 15),
+                                           lead + ((su + 3) >> 4), 64);
+                const uint32_t b6 = __shfl(pick_byte(d[u][0], (su + 6) & 15),
+                                           lead + ((su + 6) >> 4), 64);
+                ph = pseudo_hdr(b0, b2, b3, b6);
+            }
+            const int rs = (int)ph.hl, re = (int)plen[u];
+
+            uint32_t E = 0, O = 0, Eh = 0, Oh = 0;
+#pragma unroll
+            for (int c = 0; c < CPL; ++c)
+                accum_strided<KIND, FULL, HDR>(d[u][c], 16 * (gl + c * G) - s[u], rs, re,
+                                               (uint32_t)(gl + c * G) < nch[u], ph.v4, E, O,
+                                               Eh, Oh);
+            // Packets longer than one pass (e.g. 9000 B jumbo frames).
+            for (uint32_t kb = PASS; kb < nch[u]; kb += PASS) {
+                u32x4 t[CPL];
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) {
+                    const uint32_t k = kb + (uint32_t)(gl + c * G);
+                    t[c] = load_chunk<NT>(k < nch[u] ? c0[u] + 16ull * k : zero);
+                }
+#pragma unroll
+                for (int c = 0; c < CPL; ++c)
+                    accum_strided<KIND, FULL, HDR>(t[c], 16 * (int)(kb + gl + c * G) - s[u],
+                                                   rs, re, kb + (uint32_t)(gl + c * G) < nch[u],
+                                                   ph.v4, E, O, Eh, Oh);
+            }
+
+            uint32_t S = combine(E, O, s[u] & 1);
+            S += gl == 0 ? ph.special : 0u;
+            S = group_sum<G>(S);
+            uint32_t Sh = 0;
+            if constexpr (HDR)
+                Sh = group_sum<G>(combine(Eh, Oh, s[u] & 1));
+            if (gl == 0 && valid[u]) {
+                const uint64_t i = p0 + (uint64_t)u * GPW + grp;
+                const uint16_t r = fold_not(S);
+                if (out)
+                    out[i] = r;
+                nbad += r != 0;
+                if constexpr (HDR)
+                    out_hdr[i] = ph.v4 ? fold_not(Sh) : 0; // ip4.c:110-115
+            }
+        }
+    }
+
+    if (bad) {
+        // Wave-level total of the leaders' counts, one atomic per wave.
+        nbad = group_sum<64>(nbad);
+        if (lane == 0 && nbad)
+            atomicAdd(bad, (unsigned long long)nbad);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Launch table.
+
+template <int G, int CPL, int U, int KIND, bool FULL, bool NT, bool HDR = false,
+          bool RAGGED = false>
+static hipError_t launch_one(const LaunchArgs &a, int grid, hipStream_t st)
+{
+    hipLaunchKernelGGL((k_cksum<G, CPL, U, KIND, FULL, NT, HDR, RAGGED>), dim3(grid),
+                       dim3(256), 0, st, (const uint8_t *)a.base, a.stride, a.len, a.offs,
+                       a.lens, a.n, a.out, (unsigned long long *)a.bad, a.out_hdr, a.variant);
+    return hipGetLastError();
+}
+
+template <int G, int CPL, int U>
+static hipError_t launch_shape(const LaunchArgs &a, int grid, hipStream_t st)
+{
+    const bool nt = a.nontemporal;
+    if (a.kind == WC_KIND_PAYLOAD && a.out_hdr)
+        return nt ? launch_one<G, CPL, U, WC_KIND_PAYLOAD, false, true, true>(a, grid, st)
+                  : launch_one<G, CPL, U, WC_KIND_PAYLOAD, false, false, true>(a, grid, st);
+    if (a.kind == WC_KIND_PAYLOAD)
+        return nt ? launch_one<G, CPL, U, WC_KIND_PAYLOAD, false, true>(a, grid, st)
+                  : launch_one<G, CPL, U, WC_KIND_PAYLOAD, false, false>(a, grid, st);
+    if (a.full)
+        return nt ? launch_one<G, CPL, U, WC_KIND_IP, true, true>(a, grid, st)
+                  : launch_one<G, CPL, U, WC_KIND_IP, true, false>(a, grid, st);
+    return nt ? launch_one<G, CPL, U, WC_KIND_IP, false, true>(a, grid, st)
+              : launch_one<G, CPL, U, WC_KIND_IP, false, false>(a, grid, st);
+}
+
+template <int G, int CPL, int U>
+static hipError_t launch_ragged_shape(const LaunchArgs &a, int grid, hipStream_t st)
+{
+    if (a.kind == WC_KIND_PAYLOAD)
+        return launch_one<G, CPL, U, WC_KIND_PAYLOAD, false, true, false, true>(a, grid, st);
+    return launch_one<G, CPL, U, WC_KIND_IP, false, true, false, true>(a, grid, st);
+}
+
+hipError_t launch_cksum(const LaunchArgs &a, const Shape &sh, int grid, hipStream_t st)
+{
+    if (a.ragged) {
+        if (a.out_hdr)
+            return hipErrorInvalidValue;
+#define WC_SHAPE(G_, C_, U_)                                                   \
+    if (sh.group == G_ && sh.cpl == C_ && sh.unroll == U_)                     \
+        return launch_ragged_shape<G_, C_, U_>(a, grid, st);
+        WC_RAGGED_SHAPE_LIST
+#undef WC_SHAPE
+        return hipErrorInvalidValue;
+    }
+#define WC_SHAPE(G_, C_, U_)                                                   \
+    if (sh.group == G_ && sh.cpl == C_ && sh.unroll == U_)                     \
+        return launch_shape<G_, C_, U_>(a, grid, st);
+    WC_SHAPE_LIST
+#undef WC_SHAPE
+    return hipErrorInvalidValue;
+}
+
+} // namespace wc
