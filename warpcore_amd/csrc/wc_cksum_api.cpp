@@ -174,8 +174,11 @@ wc::Shape shape_for_chunks(uint32_t nch)
         return {4, 2, 2};
     if (nch <= 8)
         return {8, 1, 4};
-    if (nch <= 16)
-        return {16, 1, 4};
+    // 9..24 chunks: 8 lanes x 3 chunks, two packets per group -- fewer dead
+    // lane slots than 16 x 2 (tools/sweep_mid.sh: 256 B 78.7 -> 84.1 %,
+    // 200 B 55 -> 67.5 %, 256 B at +14 50 -> 60 % of HBM peak)
+    if (nch <= 24)
+        return {8, 3, 2};
     if (nch <= 32)
         return {16, 2, 4};
     if (nch <= 48)

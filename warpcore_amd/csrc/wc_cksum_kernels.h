@@ -20,6 +20,9 @@
     WC_SHAPE(4, 2, 4)                                                          \
     WC_SHAPE(8, 1, 2)                                                          \
     WC_SHAPE(8, 2, 4)                                                          \
+    WC_SHAPE(8, 3, 2)                                                          \
+    WC_SHAPE(8, 3, 4)                                                          \
+    WC_SHAPE(4, 5, 4)                                                          \
     WC_SHAPE(16, 1, 2)                                                         \
     WC_SHAPE(4, 1, 16)                                                         \
     WC_SHAPE(8, 1, 4)                                                          \
