@@ -122,7 +122,7 @@ def test_strided_sweep(gpu, length):
 
 @pytest.mark.parametrize("sseg", ["0", "1", "2"])
 @pytest.mark.parametrize("length", [1, 2, 15, 16, 17, 63, 64, 65, 100, 111, 128, 255, 256, 257,
-                                    576, 577, 767, 768, 1472, 1500, 9000])
+                                    400, 500, 512, 513, 576, 577, 767, 768, 1472, 1500, 9000])
 def test_strided_packed_seg(gpu, monkeypatch, length, sseg):
     """Packed strided batches (stride = len .. len + len / 8) through the seg
     kernel with computed offsets (WC_STRIDED_SEG: 0 = group kernel only,

@@ -179,10 +179,15 @@ wc::Shape shape_for_chunks(uint32_t nch)
     // 200 B 55 -> 67.5 %, 256 B at +14 50 -> 60 % of HBM peak)
     if (nch <= 24)
         return {8, 3, 2};
-    if (nch <= 32)
+    if (nch <= 30)
         return {16, 2, 4};
+    // ~512 B: 8 lanes x 6 chunks, one packet per group (85 -> 90.8 % packed,
+    // 81 -> 87 % in 2048-B slots); 576 B: (16,3,2) (85 -> 86.6 %)
+    // (profiles/sweep_r01_mid_shapes.log)
+    if (nch <= 34)
+        return {8, 6, 1};
     if (nch <= 48)
-        return {16, 3, 4};
+        return {16, 3, 2};
     if (nch <= 96)
         return {16, 6, 4};
     if (nch <= 128)

@@ -23,6 +23,10 @@
     WC_SHAPE(8, 3, 2)                                                          \
     WC_SHAPE(8, 3, 4)                                                          \
     WC_SHAPE(4, 5, 4)                                                          \
+    WC_SHAPE(8, 5, 2)                                                          \
+    WC_SHAPE(8, 6, 2)                                                          \
+    WC_SHAPE(8, 6, 1)                                                          \
+    WC_SHAPE(16, 3, 2)                                                         \
     WC_SHAPE(16, 1, 2)                                                         \
     WC_SHAPE(4, 1, 16)                                                         \
     WC_SHAPE(8, 1, 4)                                                          \
