@@ -59,7 +59,10 @@ def parse():
     ap.add_argument("--total-packets", type=int, default=1 << 28, help="c5 total")
     ap.add_argument("--window-packets", type=int, default=1 << 25, help="c5 resident window")
     ap.add_argument("--packets", type=int, default=1 << 20)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="total CPU-baseline time budget (all-thread + 1-core trials)")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="threads for the all-core CPU baseline (default: the box's share)")
     ap.add_argument("--warmup-seconds", type=float, default=0.3,
                     help="keep warming up (untimed) until this long has passed, so the "
                          "GPU clock has ramped from idle before the timed steps")
@@ -68,22 +71,59 @@ def parse():
     return ap.parse_args()
 
 
+def resolve_launch(args, env=None):
+    """How this process runs (decided before anything touches the GPU):
+    ("spawn", N) -- `--gpus N > 1` without a torchrun environment: start N
+    fresh ranks as children; ("rank", world) -- run as one rank of `world`.
+    Raises SystemExit if a torchrun world disagrees with --gpus."""
+    env = os.environ if env is None else env
+    if args.gpus < 1:
+        raise SystemExit(f"--gpus must be >= 1, not {args.gpus}")
+    if "WORLD_SIZE" not in env:
+        return ("spawn", args.gpus) if args.gpus > 1 else ("rank", 1)
+    world = int(env["WORLD_SIZE"])
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: refusing to "
+                         f"report a {world}-rank run as {args.gpus} GPUs")
+    return "rank", world
+
+
+def spawn_ranks(n, argv):
+    """Run this bench as n ranks (one process per GPU) under
+    torch.distributed.run and relay its exit code; rank 0's JSON line goes
+    straight to our stdout.  The parent never initialises the GPU and never
+    re-execs itself: the ranks are fresh child processes."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           "--nproc-per-node", str(n), "--master-addr", "127.0.0.1",
+           "--master-port", str(port), str(Path(__file__).resolve()), *argv]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.run(cmd, env=env).returncode
+
+
 def dist_setup(args):
     """One process per GPU (torchrun env).  Backend "nccl" = RCCL over xGMI;
     WC_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs (tests only)."""
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    _, world = resolve_launch(args)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and "WORLD_SIZE" in os.environ:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     ndev = torch.cuda.device_count()
+    backend = os.environ.get("WC_DIST_BACKEND", "nccl")
+    if world > 1 and backend == "nccl" and ndev < world:
+        raise SystemExit(f"{world} ranks over RCCL need {world} GPUs, {ndev} visible "
+                         "(WC_DIST_BACKEND=gloo rehearses ranks sharing a GPU)")
     dev_index = local % max(ndev, 1)
     torch.cuda.set_device(dev_index)
     coll_dev = torch.device("cuda", dev_index)
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = os.environ.get("WC_DIST_BACKEND", "nccl")
         if backend == "nccl":
             dist.init_process_group("nccl", rank=rank, world_size=world,
                                     device_id=torch.device("cuda", dev_index))
@@ -154,8 +194,10 @@ def make_workload(args, dev, rank, world):
             synth.stamp_udp_headers(buf, d_off, d_len)
         out = torch.empty(n, dtype=torch.uint16, device=dev)
 
+        wc.cksum_ragged(buf, d_off, d_len, out=out, kind=kind)  # validates the layout once
+
         def step():
-            wc.cksum_ragged(buf, d_off, d_len, out=out, kind=kind)
+            wc.cksum_ragged(buf, d_off, d_len, out=out, kind=kind, check=False)
 
         desc = (f"netmap RX ring: {n} x {L} B IP packets in {slot}-B slots at +{at}, "
                 f"ragged batch")
@@ -178,8 +220,10 @@ def make_workload(args, dev, rank, world):
         synth.stamp_udp_headers(buf, d_off, d_len)
     out = torch.empty(n, dtype=torch.uint16, device=dev)
 
+    wc.cksum_ragged(buf, d_off, d_len, out=out, kind=kind)  # validates the layout once
+
     def step():
-        wc.cksum_ragged(buf, d_off, d_len, out=out, kind=kind)
+        wc.cksum_ragged(buf, d_off, d_len, out=out, kind=kind, check=False)
 
     desc = f"C4: {n} packets, Zipf(s=1) lengths 64-1472 B (mean {nbytes / n:.1f}), packed"
     meta = {"packets_per_gpu": n, "mean_packet_bytes": round(nbytes / n, 2),
@@ -196,45 +240,77 @@ def make_workload(args, dev, rank, world):
     return step, n, nbytes, buf, out, plan, desc, meta, (offs, lens), "weak"
 
 
+def cpu_threads(args):
+    """Host threads for the all-core CPU baseline: --cpu-threads, else the
+    box's CPU share (OMP_NUM_THREADS, which the GPU box sets to its per-GPU
+    share), else every core this process may run on."""
+    try:
+        visible = len(os.sched_getaffinity(0))
+    except AttributeError:
+        visible = os.cpu_count() or 1
+    if args.cpu_threads > 0:
+        return args.cpu_threads, visible, "--cpu-threads"
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    if share.isdigit() and 0 < int(share) < visible:
+        return int(share), visible, "OMP_NUM_THREADS (the box's CPU share)"
+    return visible, visible, "sched_getaffinity"
+
+
 def cpu_baseline(args, buf, shape, nbytes_total):
-    """The oracle's C restatement timed on this host's cores (bounded sample)."""
+    """The oracle's C restatement (reference Release flags -Ofast
+    -march=native, one call per packet) timed on this host's cores on a
+    bounded sample: all threads and 1 core, best of 5 trials each
+    (BASELINE.md section 3)."""
     from oracle import c_oracle  # checker / baseline only
 
-    threads = c_oracle.default_threads()
+    threads, visible, why = cpu_threads(args)
     k = 1 if args.kind == "payload" else 0
+    trials = 5
+    per_trial = max(args.cpu_seconds / (2 * trials), 0.05)
     if args.config in ("c2", "c3", "c5"):
         L, stride = shape
-        # The whole batch (DRAM-resident on the host, far beyond its L3),
-        # repeated for >= --cpu-seconds.
+        # The whole batch (DRAM-resident on the host, far beyond its L3).
         n_s = max(1, min(args.packets, (2 << 30) // L))
         sample = buf[: n_s * stride].cpu().numpy()
-        bps, passes = c_oracle.bench_strided(sample, stride, L, n_s, kind=k,
-                                             threads=threads, min_seconds=args.cpu_seconds)
-        desc = (f"{n_s} packets x {L} B ({n_s * L / 1e9:.2f} GB, the full batch), "
-                f"{passes} passes")
+
+        def trial(th):
+            bps, passes = c_oracle.bench_strided(sample, stride, L, n_s, kind=k, threads=th,
+                                                 min_seconds=per_trial)
+            return bps, passes
+        desc = f"{n_s} packets x {L} B ({n_s * L / 1e9:.2f} GB, the full batch)"
     else:
         offs, lens = shape
         n_s = min(offs.size, 1 << 22)
         end = int(offs[n_s - 1]) + max(int(lens[n_s - 1]), 40)
         sample = buf[:end].cpu().numpy()
-        t0 = time.perf_counter()
-        passes = 0
-        while True:
-            c_oracle.cksum_ragged(sample, offs[:n_s], lens[:n_s], kind=k, threads=threads)
-            passes += 1
-            if time.perf_counter() - t0 >= args.cpu_seconds:
-                break
-        bps = passes * float(lens[:n_s].astype(np.uint64).sum()) / (time.perf_counter() - t0)
+        o_s, l_s = offs[:n_s], lens[:n_s]
+        sbytes = float(l_s.astype(np.uint64).sum())
+
+        def trial(th):
+            t0 = time.perf_counter()
+            passes = 0
+            while True:
+                c_oracle.cksum_ragged(sample, o_s, l_s, kind=k, threads=th)
+                passes += 1
+                dt = time.perf_counter() - t0
+                if dt >= per_trial:
+                    return passes * sbytes / dt, passes
         desc = (f"first {n_s} {'Zipf ' if args.config == 'c4' else ''}packets "
-                f"({end / 1e6:.0f} MB), {passes} passes")
+                f"({end / 1e6:.0f} MB)")
+    best_all = max(trial(threads)[0] for _ in range(trials))
+    best_one = max(trial(1)[0] for _ in range(trials))
     try:
         model = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo")
                      if l.startswith("model name"))
     except (OSError, StopIteration):
         model = "unknown"
-    return {"value": round(bps / GIB, 3), "unit": "GiB/s", "cores": threads,
-            "kind": "port", "sample": f"{desc}; oracle/wc_oracle.c -Ofast -march=native, "
-            f"one call per packet, {threads} pthreads on {model}"}
+    return {"value": round(best_all / GIB, 3), "unit": "GiB/s", "cores": threads,
+            "kind": "port", "value_1core": round(best_one / GIB, 3), "best_of": trials,
+            "cores_visible": visible,
+            "sample": f"{desc}, >= {per_trial:.2f} s per trial; oracle/wc_oracle.c -Ofast "
+                      f"-march=native (reference Release flags), one call per packet, "
+                      f"{threads} pthreads ({why}; {visible} cores visible) and 1 core, "
+                      f"best of {trials} each, on {model}"}
 
 
 def last_count(args):
@@ -272,6 +348,9 @@ def parity_check(args, buf, out, shape, nbytes):
 
 def main():
     args = parse()
+    how, n_ranks = resolve_launch(args)
+    if how == "spawn":
+        return spawn_ranks(n_ranks, sys.argv[1:])
     from warpcore_amd import dist as wdist
     rank, local, world, coll_dev = dist_setup(args)
     dev = torch.device("cuda", local)
@@ -306,7 +385,11 @@ def main():
     kernel_ms_max = wdist.max_over_ranks(kernel_ms, coll_dev)
     total_bytes = float(wdist.sum_over_ranks(int(nbytes), coll_dev)) * args.steps
     value = total_bytes / elapsed / GIB
-    achieved = nbytes / (kernel_ms * 1e-3) / 1e9  # GB/s of payload per launch (rank-local)
+    # Roofline of the dominant kernel: one rank's algorithmic bytes per launch
+    # over the slowest rank's average launch time (all ranks move the same
+    # bytes); frac_job is the whole job's rate against N x peak.
+    achieved = nbytes / (kernel_ms_max * 1e-3) / 1e9
+    frac_job = value * GIB / 1e9 / (world * HBM_PEAK_GBPS)
 
     parity = parity_check(args, buf, out, shape, nbytes)
     parity["checked_packets"] = wdist.sum_over_ranks(parity["checked_packets"], coll_dev)
@@ -333,6 +416,7 @@ def main():
                   "ranks_mismatched": wdist.sum_over_ranks(bad, coll_dev)}
 
     traffic = None
+    traffic_source = None
     try:
         tf = json.loads(Path(args.traffic_file).read_text())
         key = f"{args.config}:{meta.get('packet_bytes', 'zipf')}"
@@ -342,6 +426,9 @@ def main():
             key += ":headers"
         if key in tf:
             traffic = tf[key]["hbm_bytes_per_launch"]
+            traffic_source = (f"{os.path.relpath(args.traffic_file, ROOT)} [{key}] "
+                              f"({tf[key].get('round', 'r01')}: rocprofv3 --pmc FETCH_SIZE x2 + "
+                              f"WRITE_SIZE, separate passes; a static lookup, not this run)")
     except (OSError, ValueError, KeyError):
         traffic = None
 
@@ -370,7 +457,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                         "traffic": traffic,
+                         "traffic": traffic, "traffic_source": traffic_source,
+                         "frac_job": round(frac_job, 4),
                          "kernel_ms_avg": round(kernel_ms, 5),
                          "kernel_ms_avg_max_rank": round(kernel_ms_max, 5)},
             "cpu_baseline": cpu,
@@ -386,4 +474,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

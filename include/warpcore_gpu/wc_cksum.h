@@ -116,8 +116,14 @@ int wc_host_unregister(void *h_ptr);
  * (staging ring, streams).  Called implicitly by every entry point with
  * device -1 ("current device"); calling it explicitly is optional. */
 int wc_gpu_init(int device);
-/* Release the scratch created by wc_gpu_init. */
+/* Release the scratch created by wc_gpu_init, and every page-lock taken by
+ * wc_host_register (register again after a re-init). */
 int wc_gpu_fini(void);
+
+/* The WC_* tuning environment (kernel shapes, path choices) is
+ * read once, at the first initialisation.  Re-read it now (A/B tuning tools
+ * and tests; never needed in production). */
+int wc_config_reload(void);
 
 /* Counter-based synthetic packet bytes (bench / tests): little-endian 8-byte
  * word k of [d_buf, d_buf + nbytes) is splitmix64 output k for `seed`. */

@@ -28,3 +28,14 @@ def gpu():
     import warpcore_amd
     warpcore_amd.gpu_init(0)
     return torch.device("cuda:0")
+
+
+@pytest.fixture(autouse=True)
+def _fresh_wc_config():
+    """libwccksum reads its WC_* tuning environment once; a test that
+    monkeypatches it calls wc.reload_config(), and every test starts from the
+    (restored) environment of the session."""
+    from warpcore_amd import _lib
+    if _lib._lib is not None:
+        _lib._lib.wc_config_reload()
+    yield

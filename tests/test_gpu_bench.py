@@ -72,3 +72,55 @@ def test_bench_other_configs(gpu, args):
     line = _last_json(r.stdout)
     assert line["value"] > 0 and line["parity"]["mismatches"] == 0
     assert line["parity"]["checked_packets"] == line["config"]["packets_per_gpu"]
+
+
+def test_bench_spawns_ranks_without_torchrun(gpu):
+    """`bench.py --gpus 2` with no torchrun environment starts 2 ranks itself
+    (the driver's command shape); gloo so both ranks can share cuda:0."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["WC_DIST_BACKEND"] = "gloo"
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2",
+                        "--steps", "5", "--warmup", "1", "--packets", "65536"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = _last_json(r.stdout)
+    assert line["n_gpus"] == 2
+    assert line["parity"] == {"checked_packets": 2 * 65536, "mismatches": 0}
+    assert line["results_allgather"]["ranks_mismatched"] == 0
+    assert 0 < line["roofline"]["frac_job"] < 1.5
+
+
+def test_bench_c5_windowed(gpu):
+    """SURVEY C5's 1-GPU shape at reduced size: 2^22 x 1472 B as 4 launches
+    over a resident 2^20-packet window, the last window checked in full."""
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--config", "c5",
+                        "--total-packets", str(1 << 22), "--window-packets", str(1 << 20),
+                        "--steps", "3", "--warmup", "1", "--cpu-seconds", "0.5"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = _last_json(r.stdout)
+    assert line["scaling"] == "strong"
+    assert line["config"]["launches_per_step"] == 4
+    assert line["config"]["packets_per_gpu"] == 1 << 22
+    assert line["parity"] == {"checked_packets": 1 << 20, "mismatches": 0}
+    assert line["cpu_baseline"]["best_of"] == 5 and line["cpu_baseline"]["value_1core"] > 0
+
+
+def test_bench_c5_two_rank_split(gpu):
+    """The same strong-scaling split rehearsed at 2 ranks (gloo, sharing
+    cuda:0): each rank takes half of the total as 2 launches over its own
+    window, checked on every rank."""
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["WC_DIST_BACKEND"] = "gloo"
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2", "--config", "c5",
+                        "--total-packets", str(1 << 22), "--window-packets", str(1 << 20),
+                        "--steps", "3", "--warmup", "1"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = _last_json(r.stdout)
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong"
+    assert line["config"]["launches_per_step"] == 2
+    assert line["config"]["packets_per_gpu"] == 1 << 21
+    assert line["parity"] == {"checked_packets": 2 << 20, "mismatches": 0}

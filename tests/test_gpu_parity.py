@@ -55,6 +55,7 @@ def ragged_mode(monkeypatch, mode: str) -> None:
         monkeypatch.delenv(k, raising=False)
     for k, v in RAGGED_MODES[mode].items():
         monkeypatch.setenv(k, v)
+    wc.reload_config()  # the library reads WC_* once; re-read for this test
 
 
 # ---------------------------------------------------------------------------
@@ -129,6 +130,7 @@ def test_strided_packed_seg(gpu, monkeypatch, length, sseg):
     1 = planner default, 2 = seg kernel whenever packed): several tiles and
     a partial one, every start phase, ip_cksum and payload_cksum."""
     monkeypatch.setenv("WC_STRIDED_SEG", sseg)
+    wc.reload_config()
     rng = np.random.default_rng(length * 7 + int(sseg))
     n = 150
     for stride in sorted({length, length + 1, length + length // 8}):
@@ -244,6 +246,7 @@ def test_ragged_group_kernel(gpu, monkeypatch, shape):
     and empty packets, and wild IPv4/IPv6 packets at odd alignment."""
     monkeypatch.setenv("WC_FLAT_MIN", str(1 << 40))
     monkeypatch.setenv("WC_RAGGED_SHAPE", shape)
+    wc.reload_config()
     g = np.load(GOLDEN / "vectors.npz")
     for k, pre in ((0, "ip"), (1, "pl")):
         out = wc.cksum_ragged(dev_u8(g[pre + "_blob"], gpu), to_dev(g[pre + "_off"], gpu),

@@ -38,6 +38,7 @@ def main() -> None:
             ref = None
             for path, zc in (("zero-copy", str(1 << 30)), ("pipeline", "0")):
                 os.environ["WC_ZC_BYTES"] = zc
+                wc.reload_config()
                 for _ in range(20):
                     out = wc.cksum_host(pool, offs, lens)
                 t = []

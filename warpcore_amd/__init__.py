@@ -7,13 +7,13 @@ packet generators and the multi-GPU shard driver used by bench.py.
 """
 from .cksum import (KIND_IP, KIND_PAYLOAD, WcError, cksum_host, cksum_ip_udp_ragged,
                     cksum_ip_udp_strided, cksum_ragged, cksum_strided, gpu_init, host_register, host_unregister,
-                    ip_cksum, payload_cksum, plan_strided, synth_fill,
+                    ip_cksum, payload_cksum, plan_strided, reload_config, synth_fill,
                     verify_ragged, verify_strided, version)
 
 __all__ = [
     "KIND_IP", "KIND_PAYLOAD", "WcError", "cksum_host", "cksum_ip_udp_ragged",
     "cksum_ip_udp_strided", "cksum_ragged",
     "cksum_strided", "gpu_init", "host_register", "host_unregister", "ip_cksum",
-    "payload_cksum", "plan_strided", "synth_fill", "verify_ragged",
+    "payload_cksum", "plan_strided", "reload_config", "synth_fill", "verify_ragged",
     "verify_strided", "version",
 ]

@@ -53,9 +53,9 @@ def _kind(kind) -> int:
         raise ValueError(f"kind must be 'ip' or 'payload', not {kind!r}") from None
 
 
-def _stream_ptr(stream) -> int:
+def _stream_ptr(stream, device=None) -> int:
     if stream is None:
-        return torch.cuda.current_stream().cuda_stream
+        return torch.cuda.current_stream(device).cuda_stream
     if isinstance(stream, torch.cuda.Stream):
         return stream.cuda_stream
     return int(stream)
@@ -67,6 +67,105 @@ def _dev_ptr(t: Union[torch.Tensor, int]) -> int:
             raise ValueError("batch buffers must be device (cuda) tensors")
         return t.data_ptr()
     return int(t)
+
+
+def reload_config() -> None:
+    """Re-read the WC_* tuning environment (read once at first init)."""
+    _check("wc_config_reload", _lib.load().wc_config_reload())
+
+
+def _span(length: int, kind: int) -> int:
+    # payload_cksum reads the IPv4 header fields up to byte 19 whatever len is
+    # (in_cksum.c:149-151)
+    return max(length, 20) if kind == KIND_PAYLOAD else length
+
+
+def _check_len(length: int) -> int:
+    if not 0 <= int(length) <= 0xFFFF:
+        raise ValueError("len is a uint16 in the reference (0..65535)")
+    return int(length)
+
+
+def _same_device(base: torch.Tensor, **others) -> None:
+    if not isinstance(base, torch.Tensor) or not base.is_cuda:
+        raise ValueError("base must be a device (cuda) tensor")
+    for name, t in others.items():
+        if t is None:
+            continue
+        if not isinstance(t, torch.Tensor) or not t.is_cuda:
+            raise ValueError(f"{name} must be a device (cuda) tensor")
+        if t.device != base.device:
+            raise ValueError(f"{name} is on {t.device}, base on {base.device}")
+
+
+def _nbytes(t: torch.Tensor) -> int:
+    return t.numel() * t.element_size()
+
+
+def _check_strided(base: torch.Tensor, byte_offset: int, stride: int, length: int, n: int,
+                   kind: int) -> None:
+    if byte_offset < 0 or stride < 0 or n < 0:
+        raise ValueError("byte_offset, stride and n must be >= 0")
+    if not base.is_contiguous():
+        raise ValueError("base must be contiguous")
+    if n and byte_offset + (n - 1) * stride + _span(length, kind) > _nbytes(base):
+        raise ValueError(f"batch of {n} x {length} B at stride {stride} (+{byte_offset}) "
+                         f"runs past the {_nbytes(base)}-byte buffer")
+
+
+def _check_ragged(base: torch.Tensor, offsets: torch.Tensor, lengths: torch.Tensor,
+                  kind: int, check: bool) -> int:
+    _same_device(base, offsets=offsets, lengths=lengths)
+    n = _check_ragged_shapes(offsets, lengths)
+    if not base.is_contiguous():
+        raise ValueError("base must be contiguous")
+    if check and n:
+        # one device reduction + sync -- pass check=False on a hot loop whose
+        # layout was validated once
+        _ragged_bounds(_nbytes(base), offsets, lengths, kind)
+    return n
+
+
+def _check_ragged_shapes(offsets: torch.Tensor, lengths: torch.Tensor) -> int:
+    n = offsets.numel()
+    if (lengths.numel() != n or offsets.element_size() != 8 or lengths.element_size() != 2
+            or offsets.is_floating_point() or lengths.is_floating_point()):
+        raise ValueError("offsets must be 8-byte and lengths 2-byte integers, same count")
+    if not (offsets.is_contiguous() and lengths.is_contiguous()):
+        raise ValueError("offsets and lengths must be contiguous")
+    return n
+
+
+def _ragged_bounds(nbytes: int, offsets: torch.Tensor, lengths: torch.Tensor,
+                   kind: int) -> None:
+    """Every packet (and payload_cksum's 20 header bytes) inside [0, nbytes)."""
+    off = offsets.view(torch.int64)
+    ln = lengths.view(torch.int16).to(torch.int64) & 0xFFFF
+    if kind == KIND_PAYLOAD:
+        ln = torch.clamp(ln, min=20)
+    if bool((off < 0).any()) or int((off + ln).max()) > nbytes:
+        raise ValueError("a packet [off, off + len) runs past the buffer")
+
+
+class _on_device:
+    """Make base's device current for the library call (it resolves its
+    device with hipGetDevice)."""
+
+    def __init__(self, device: torch.device):
+        self.idx = device.index if device.index is not None else torch.cuda.current_device()
+        self.prev = None
+
+    def __enter__(self):
+        cur = torch.cuda.current_device()
+        if cur != self.idx:
+            self.prev = cur
+            torch.cuda.set_device(self.idx)
+        return self
+
+    def __exit__(self, *exc):
+        if self.prev is not None:
+            torch.cuda.set_device(self.prev)
+        return False
 
 
 # --------------------------------------------------------------------------
@@ -107,6 +206,8 @@ def _out_tensor(out: Optional[torch.Tensor], n: int, device) -> torch.Tensor:
         out = torch.empty(n, dtype=torch.uint16, device=device)
     if out.numel() < n or out.element_size() != 2 or not out.is_contiguous():
         raise ValueError("out must be a contiguous 2-byte tensor of >= n entries")
+    if not out.is_cuda or out.device != torch.device(device):
+        raise ValueError(f"out must be on {device}")
     return out
 
 
@@ -114,70 +215,87 @@ def cksum_strided(base: torch.Tensor, stride: int, length: int, n: int,
                   out: Optional[torch.Tensor] = None, kind="ip",
                   stream=None, byte_offset: int = 0) -> torch.Tensor:
     """Checksum packets ``base[byte_offset + i*stride : ... + length]``, i < n."""
+    k = _kind(kind)
+    _same_device(base)
+    _check_strided(base, byte_offset, stride, _check_len(length), n, k)
     out = _out_tensor(out, n, base.device)
-    _check("wc_cksum_strided", _lib.load().wc_cksum_strided(
-        _dev_ptr(base) + byte_offset, stride, length, n, out.data_ptr(),
-        _kind(kind), _stream_ptr(stream)))
+    with _on_device(base.device):
+        _check("wc_cksum_strided", _lib.load().wc_cksum_strided(
+            _dev_ptr(base) + byte_offset, stride, length, n, out.data_ptr(),
+            k, _stream_ptr(stream, base.device)))
     return out
 
 
 def cksum_ragged(base: torch.Tensor, offsets: torch.Tensor, lengths: torch.Tensor,
                  out: Optional[torch.Tensor] = None, kind="ip",
-                 stream=None) -> torch.Tensor:
-    """Checksum packets ``base[off[i] : off[i] + len[i]]`` (uint64 / uint16 arrays)."""
-    n = offsets.numel()
-    if lengths.numel() != n or offsets.element_size() != 8 or lengths.element_size() != 2:
-        raise ValueError("offsets must be 8-byte and lengths 2-byte, same count")
+                 stream=None, check: bool = True) -> torch.Tensor:
+    """Checksum packets ``base[off[i] : off[i] + len[i]]`` (uint64 / uint16
+    arrays).  ``check`` validates every packet against ``base`` (one device
+    reduction and a sync); pass False on a loop over an already-checked
+    layout."""
+    k = _kind(kind)
+    n = _check_ragged(base, offsets, lengths, k, check)
     out = _out_tensor(out, n, base.device)
-    _check("wc_cksum_ragged", _lib.load().wc_cksum_ragged(
-        _dev_ptr(base), _dev_ptr(offsets), _dev_ptr(lengths), n, out.data_ptr(),
-        _kind(kind), _stream_ptr(stream)))
+    with _on_device(base.device):
+        _check("wc_cksum_ragged", _lib.load().wc_cksum_ragged(
+            _dev_ptr(base), _dev_ptr(offsets), _dev_ptr(lengths), n, out.data_ptr(),
+            k, _stream_ptr(stream, base.device)))
     return out
 
 
 def verify_strided(base, stride, length, n, kind="payload", out=None,
-                   stream=None) -> Tuple[torch.Tensor, torch.Tensor]:
+                   stream=None, byte_offset: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
     """RX check (udp.c:132-139): results plus the count of non-zero checksums."""
+    k = _kind(kind)
+    _same_device(base)
+    _check_strided(base, byte_offset, stride, _check_len(length), n, k)
     out = _out_tensor(out, n, base.device)
     bad = torch.zeros(1, dtype=torch.int64, device=base.device)
-    _check("wc_verify_strided", _lib.load().wc_verify_strided(
-        _dev_ptr(base), stride, length, n, out.data_ptr(), bad.data_ptr(),
-        _kind(kind), _stream_ptr(stream)))
+    with _on_device(base.device):
+        _check("wc_verify_strided", _lib.load().wc_verify_strided(
+            _dev_ptr(base) + byte_offset, stride, length, n, out.data_ptr(), bad.data_ptr(),
+            k, _stream_ptr(stream, base.device)))
     return out, bad
 
 
 def verify_ragged(base, offsets, lengths, kind="payload", out=None,
-                  stream=None) -> Tuple[torch.Tensor, torch.Tensor]:
-    n = offsets.numel()
+                  stream=None, check: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
+    k = _kind(kind)
+    n = _check_ragged(base, offsets, lengths, k, check)
     out = _out_tensor(out, n, base.device)
     bad = torch.zeros(1, dtype=torch.int64, device=base.device)
-    _check("wc_verify_ragged", _lib.load().wc_verify_ragged(
-        _dev_ptr(base), _dev_ptr(offsets), _dev_ptr(lengths), n, out.data_ptr(),
-        bad.data_ptr(), _kind(kind), _stream_ptr(stream)))
+    with _on_device(base.device):
+        _check("wc_verify_ragged", _lib.load().wc_verify_ragged(
+            _dev_ptr(base), _dev_ptr(offsets), _dev_ptr(lengths), n, out.data_ptr(),
+            bad.data_ptr(), k, _stream_ptr(stream, base.device)))
     return out, bad
 
 
 def cksum_ip_udp_strided(base: torch.Tensor, stride: int, length: int, n: int,
-                        stream=None, byte_offset: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
+                         stream=None, byte_offset: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
     """One pass over IP/UDP packets: (IPv4 header checksums, payload_cksum).
     The header checksum is ip_cksum(ip, ip4_hl) (ip4.c:110-115, 184-186); 0
     for IPv6 packets."""
+    _same_device(base)
+    _check_strided(base, byte_offset, stride, _check_len(length), n, KIND_PAYLOAD)
     hdr = _out_tensor(None, n, base.device)
     pay = _out_tensor(None, n, base.device)
-    _check("wc_cksum_ip_udp_strided", _lib.load().wc_cksum_ip_udp_strided(
-        _dev_ptr(base) + byte_offset, stride, length, n, hdr.data_ptr(), pay.data_ptr(),
-        _stream_ptr(stream)))
+    with _on_device(base.device):
+        _check("wc_cksum_ip_udp_strided", _lib.load().wc_cksum_ip_udp_strided(
+            _dev_ptr(base) + byte_offset, stride, length, n, hdr.data_ptr(), pay.data_ptr(),
+            _stream_ptr(stream, base.device)))
     return hdr, pay
 
 
 def cksum_ip_udp_ragged(base: torch.Tensor, offsets: torch.Tensor, lengths: torch.Tensor,
-                        stream=None) -> Tuple[torch.Tensor, torch.Tensor]:
-    n = offsets.numel()
+                        stream=None, check: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
+    n = _check_ragged(base, offsets, lengths, KIND_PAYLOAD, check)
     hdr = _out_tensor(None, n, base.device)
     pay = _out_tensor(None, n, base.device)
-    _check("wc_cksum_ip_udp_ragged", _lib.load().wc_cksum_ip_udp_ragged(
-        _dev_ptr(base), _dev_ptr(offsets), _dev_ptr(lengths), n, hdr.data_ptr(),
-        pay.data_ptr(), _stream_ptr(stream)))
+    with _on_device(base.device):
+        _check("wc_cksum_ip_udp_ragged", _lib.load().wc_cksum_ip_udp_ragged(
+            _dev_ptr(base), _dev_ptr(offsets), _dev_ptr(lengths), n, hdr.data_ptr(),
+            pay.data_ptr(), _stream_ptr(stream, base.device)))
     return hdr, pay
 
 
@@ -191,8 +309,16 @@ def cksum_host(buf: np.ndarray, offsets: np.ndarray, lengths: np.ndarray,
     Small batches in a registered buffer are read in place by one kernel;
     larger ones are streamed over pinned H2D copies (wc_cksum_host)."""
     buf = np.ascontiguousarray(buf).reshape(-1).view(np.uint8)
-    off = np.ascontiguousarray(offsets, dtype=np.uint64)
-    lens = np.ascontiguousarray(lengths, dtype=np.uint16)
+    lens_in = np.asarray(lengths)
+    if lens_in.size and (lens_in.min() < 0 or lens_in.max() > 0xFFFF):
+        raise ValueError("len is a uint16 in the reference (0..65535)")
+    offs_in = np.asarray(offsets)
+    if offs_in.size and offs_in.dtype.kind == "i" and offs_in.min() < 0:
+        raise ValueError("negative offset")
+    if offs_in.shape != lens_in.shape:
+        raise ValueError("offsets and lengths must have the same shape")
+    off = np.ascontiguousarray(offs_in, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens_in, dtype=np.uint16)
     out = np.empty(off.size, dtype=np.uint16)
     _check("wc_cksum_host", _lib.load().wc_cksum_host(
         buf.ctypes.data, buf.size, off.ctypes.data, lens.ctypes.data, off.size,
@@ -214,9 +340,13 @@ def host_unregister(buf: np.ndarray) -> None:
 def synth_fill(buf: torch.Tensor, seed: int, nbytes: Optional[int] = None,
                stream=None) -> torch.Tensor:
     """Fill a device buffer with the counter-based splitmix64 byte stream."""
-    nbytes = buf.numel() * buf.element_size() if nbytes is None else nbytes
-    _check("wc_synth_fill", _lib.load().wc_synth_fill(
-        _dev_ptr(buf), nbytes, seed & 0xFFFFFFFFFFFFFFFF, _stream_ptr(stream)))
+    _same_device(buf)
+    nbytes = _nbytes(buf) if nbytes is None else nbytes
+    if not 0 <= nbytes <= _nbytes(buf):
+        raise ValueError(f"nbytes {nbytes} outside the {_nbytes(buf)}-byte buffer")
+    with _on_device(buf.device):
+        _check("wc_synth_fill", _lib.load().wc_synth_fill(
+            _dev_ptr(buf), nbytes, seed & 0xFFFFFFFFFFFFFFFF, _stream_ptr(stream, buf.device)))
     return buf
 
 

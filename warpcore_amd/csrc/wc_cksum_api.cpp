@@ -81,9 +81,41 @@ struct Registration {
     const uint8_t *dptr; // device address of the region's first byte
 };
 
+// Tuning knobs (the WC_* environment), read once when the library first
+// initialises and again only on wc_config_reload(); the defaults are the
+// values tuned on MI355X (DESIGN.md sections 4-5).  Batch calls take a copy
+// under g_mu, so a reload never races a launch.
+struct Config {
+    int blocks_per_cu = 0;         // WC_BLOCKS_PER_CU: cap the one-shot grid
+    int grid = 0;                  // WC_GRID: fixed grid (grid-stride)
+    int variant = 0;               // WC_VARIANT: experimental kernel variants
+    bool have_shape = false;       // WC_SHAPE=G,CPL,U: force the strided shape
+    wc::Shape shape{};
+    bool have_rshape = false;      // WC_RAGGED_SHAPE: small ragged group shape
+    wc::Shape rshape{};
+    int strided_seg = 1;           // WC_STRIDED_SEG: 0 never, 1 by size, 2 always
+    int sseg_minch = 7;            // WC_STRIDED_SEG_MINCH
+    int sseg_maxch = 48;           // WC_STRIDED_SEG_MAXCH
+    int flat_un = 2;               // WC_FLAT_UN: flat kernel rows per group
+    int flat_tpw = 1;              // WC_FLAT_TPW: flat kernel tiles per wave
+    int seg = 1;                   // WC_SEG: 0 = flat kernel for ragged batches
+    int seg_rows = 4;              // WC_SEG_ROWS
+    int zc_seg = 0;                // WC_ZC_SEG: seg kernel on zero-copy batches
+    int zc_group_max = (int)kZcGroupMax; // WC_ZC_GROUP_MAX
+    int zc_bytes = kZcBytesDefault;      // WC_ZC_BYTES
+    uint64_t flat_min = kFlatMinDefault; // WC_FLAT_MIN: ragged group kernel below this n
+    int diag_noload = 0;           // WC_DIAG_NOLOAD: timing-only build
+    int nt = 1;                    // WC_NT: nontemporal loads
+    int grp_dense = 65;            // WC_GRP_DENSE (64ths; 65 = never)
+    int grp_sparse = 40;           // WC_GRP_SPARSE
+    int grp_rows = 4;              // WC_GRP_ROWS
+};
+
 std::mutex g_mu;
 Device g_dev[kMaxDevices];
 std::map<uintptr_t, Registration> g_registered; // host base -> region
+Config g_cfg;
+bool g_cfg_loaded = false;
 
 int hip_err(hipError_t e) { return e == hipSuccess ? WC_OK : -(int)e; }
 
@@ -91,6 +123,49 @@ int env_int(const char *name, int dflt)
 {
     const char *v = getenv(name);
     return (v && *v) ? atoi(v) : dflt;
+}
+
+uint64_t env_u64(const char *name, uint64_t dflt)
+{
+    const char *v = getenv(name);
+    return (v && *v) ? strtoull(v, nullptr, 0) : dflt;
+}
+
+bool parse_shape(const char *v, wc::Shape *sh)
+{
+    int g = 0, c = 0, u = 0;
+    if (!v || !*v || sscanf(v, "%d,%d,%d", &g, &c, &u) != 3)
+        return false;
+    *sh = {g, c, u};
+    return true;
+}
+
+void load_config_locked()
+{
+    Config c;
+    c.blocks_per_cu = env_int("WC_BLOCKS_PER_CU", c.blocks_per_cu);
+    c.grid = env_int("WC_GRID", c.grid);
+    c.variant = env_int("WC_VARIANT", c.variant);
+    c.have_shape = parse_shape(getenv("WC_SHAPE"), &c.shape);
+    c.have_rshape = parse_shape(getenv("WC_RAGGED_SHAPE"), &c.rshape);
+    c.strided_seg = env_int("WC_STRIDED_SEG", c.strided_seg);
+    c.sseg_minch = env_int("WC_STRIDED_SEG_MINCH", c.sseg_minch);
+    c.sseg_maxch = env_int("WC_STRIDED_SEG_MAXCH", c.sseg_maxch);
+    c.flat_un = env_int("WC_FLAT_UN", c.flat_un);
+    c.flat_tpw = env_int("WC_FLAT_TPW", c.flat_tpw);
+    c.seg = env_int("WC_SEG", c.seg);
+    c.seg_rows = env_int("WC_SEG_ROWS", c.seg_rows);
+    c.zc_seg = env_int("WC_ZC_SEG", c.zc_seg);
+    c.zc_group_max = env_int("WC_ZC_GROUP_MAX", c.zc_group_max);
+    c.zc_bytes = env_int("WC_ZC_BYTES", c.zc_bytes);
+    c.flat_min = env_u64("WC_FLAT_MIN", c.flat_min);
+    c.diag_noload = env_int("WC_DIAG_NOLOAD", c.diag_noload);
+    c.nt = env_int("WC_NT", c.nt);
+    c.grp_dense = env_int("WC_GRP_DENSE", c.grp_dense);
+    c.grp_sparse = env_int("WC_GRP_SPARSE", c.grp_sparse);
+    c.grp_rows = env_int("WC_GRP_ROWS", c.grp_rows);
+    g_cfg = c;
+    g_cfg_loaded = true;
 }
 
 int current_device(int *dev)
@@ -122,6 +197,8 @@ int init_locked(int device, Device **out)
         if (rc)
             return rc;
     }
+    if (!g_cfg_loaded)
+        load_config_locked();
     Device &D = g_dev[device];
     if (!D.ok) {
         hipDeviceProp_t prop;
@@ -154,10 +231,13 @@ int init_locked(int device, Device **out)
     return WC_OK;
 }
 
-int ensure_device(Device **out)
+int ensure_device(Device **out, Config *cfg)
 {
     std::lock_guard<std::mutex> lk(g_mu);
-    return init_locked(-1, out);
+    const int rc = init_locked(-1, out);
+    if (rc == WC_OK)
+        *cfg = g_cfg;
+    return rc;
 }
 
 // ---------------------------------------------------------------------------
@@ -199,17 +279,7 @@ wc::Shape shape_for_chunks(uint32_t nch)
     return {64, 9, 1};
 }
 
-
-bool parse_shape(const char *v, wc::Shape *sh)
-{
-    int g = 0, c = 0, u = 0;
-    if (!v || !*v || sscanf(v, "%d,%d,%d", &g, &c, &u) != 3)
-        return false;
-    *sh = {g, c, u};
-    return true;
-}
-
-int grid_for(const Device &D, const wc::Shape &sh, uint64_t n)
+int grid_for(const Device &D, const Config &C, const wc::Shape &sh, uint64_t n)
 {
     const uint64_t ppw = (uint64_t)(64 / sh.group) * sh.unroll;
     const uint64_t waves = (n + ppw - 1) / ppw;
@@ -218,13 +288,13 @@ int grid_for(const Device &D, const wc::Shape &sh, uint64_t n)
     // wave and retires (measured faster than a resident grid-stride loop on
     // MI355X: DESIGN.md section 5).  WC_BLOCKS_PER_CU / WC_GRID cap it into a
     // grid-stride launch for experiments.
-    uint64_t cap = 0x7FFFFFFFull;
-    const int per_cu = env_int("WC_BLOCKS_PER_CU", 0);
-    if (per_cu > 0)
-        cap = (uint64_t)D.cus * (uint64_t)per_cu;
-    const int fixed = env_int("WC_GRID", 0);
-    if (fixed > 0)
-        cap = (uint64_t)fixed;
+    // The kernel grid-strides, so capping at wc::kMaxGridBlocks (gridDim.x *
+    // 256 must fit in a uint32) stays correct for any n.
+    uint64_t cap = wc::kMaxGridBlocks;
+    if (C.blocks_per_cu > 0)
+        cap = std::min(cap, (uint64_t)D.cus * (uint64_t)C.blocks_per_cu);
+    if (C.grid > 0)
+        cap = std::min(cap, (uint64_t)C.grid);
     return (int)std::max<uint64_t>(1, std::min(blocks, cap));
 }
 
@@ -235,19 +305,18 @@ struct Plan {
     int seg_rows = 0; // ragged: k_cksum_seg row-group size, 0 = flat kernel
 };
 
-Plan plan_strided(const Device &D, uint64_t base, uint64_t stride, uint32_t len,
-                  uint64_t n, int kind, bool hdr = false)
+Plan plan_strided(const Device &D, const Config &C, uint64_t base, uint64_t stride,
+                  uint32_t len, uint64_t n, int kind, bool hdr = false)
 {
     Plan p;
     const uint32_t span = kind == WC_CKSUM_PAYLOAD ? std::max(len, 20u) : len;
     // Worst-case start phase within a 16-byte chunk over the batch.
     const uint32_t phase = (stride % 16 == 0) ? (uint32_t)(base % 16) : 15u;
     const uint32_t nch = (phase + span + 15u) / 16u;
-    p.shape = shape_for_chunks(nch);
-    parse_shape(getenv("WC_SHAPE"), &p.shape);
+    p.shape = C.have_shape ? C.shape : shape_for_chunks(nch);
     p.full = kind == WC_CKSUM_IP && base % 16 == 0 && stride % 16 == 0 &&
-             len % 16 == 0 && !(env_int("WC_VARIANT", 0) & 2);
-    p.grid = grid_for(D, p.shape, n);
+             len % 16 == 0 && !(C.variant & 2);
+    p.grid = grid_for(D, C, p.shape, n);
     // Packed (or nearly packed) packets that the group kernel would have to
     // mask: the seg kernel streams their byte range instead (k_cksum_seg<STR>)
     // -- measured better from 7 to 48 chunks per packet (256 B at +14: 59 ->
@@ -255,13 +324,12 @@ Plan plan_strided(const Device &D, uint64_t base, uint64_t stride, uint32_t len,
     // 85 %) and for tiny packets.  WC_STRIDED_SEG = 0
     // never, 2 always (no fused header), 1 = chunk counts in
     // [WC_STRIDED_SEG_MINCH, WC_STRIDED_SEG_MAXCH].
-    const int sseg = env_int("WC_STRIDED_SEG", 1);
+    const int sseg = C.strided_seg;
     const bool packed = len != 0 && stride >= len && stride <= len + len / 8u;
-    const bool seg_size = nch >= (uint32_t)env_int("WC_STRIDED_SEG_MINCH", 7) &&
-                          nch <= (uint32_t)env_int("WC_STRIDED_SEG_MAXCH", 48);
+    const bool seg_size = nch >= (uint32_t)C.sseg_minch && nch <= (uint32_t)C.sseg_maxch;
     if (!hdr && !p.full && n >= 64 && packed && (sseg == 2 || (sseg == 1 && seg_size))) {
-        p.shape = {0, 1, env_int("WC_FLAT_UN", 2)};
-        p.seg_rows = env_int("WC_SEG_ROWS", 4);
+        p.shape = {0, 1, C.flat_un};
+        p.seg_rows = C.seg_rows;
         p.grid = 0;
     }
     return p;
@@ -278,41 +346,37 @@ Plan plan_strided(const Device &D, uint64_t base, uint64_t stride, uint32_t len,
 // kernel issues every packet's loads at once.  (Device-resident batches
 // measured no better on the group kernel at any size -- launch cost
 // dominates small ones -- so WC_FLAT_MIN defaults to 0.)
-Plan plan_ragged(const Device &D, uint64_t n, int kind, bool zero_copy = false,
-                 bool hdr = false)
+Plan plan_ragged(const Device &D, const Config &C, uint64_t n, int kind,
+                 bool zero_copy = false, bool hdr = false)
 {
     (void)D;
     Plan p;
     p.full = false;
-    const bool small =
-        (zero_copy && n <= (uint64_t)env_int("WC_ZC_GROUP_MAX", (int)kZcGroupMax)) ||
-        n < (uint64_t)env_int("WC_FLAT_MIN", kFlatMinDefault);
+    const bool small = (zero_copy && n <= (uint64_t)C.zc_group_max) ||
+                       n < C.flat_min;
     if (small && !hdr) {
-        p.shape = {64, 2, 1};
-        parse_shape(getenv("WC_RAGGED_SHAPE"), &p.shape);
+        p.shape = C.have_rshape ? C.rshape : wc::Shape{64, 2, 1};
         const uint64_t ppw = (uint64_t)(64 / p.shape.group) * p.shape.unroll;
-        p.grid = (int)std::max<uint64_t>(1, ((n + ppw - 1) / ppw + 3) / 4);
+        p.grid = (int)std::min<uint64_t>(
+            wc::kMaxGridBlocks, std::max<uint64_t>(1, ((n + ppw - 1) / ppw + 3) / 4));
         return p;
     }
-    p.shape = {0, 1, env_int("WC_FLAT_UN", 2)};
+    p.shape = {0, 1, C.flat_un};
     p.grid = 0;
-    const int seg = env_int("WC_SEG", 1);
-    if ((!zero_copy || env_int("WC_ZC_SEG", 0)) && env_int("WC_DIAG_NOLOAD", 0) == 0 && seg != 0 &&
+    if ((!zero_copy || C.zc_seg) && C.diag_noload == 0 && C.seg != 0 &&
         (!hdr || kind == WC_CKSUM_PAYLOAD))
-        p.seg_rows = env_int("WC_SEG_ROWS", 4);
+        p.seg_rows = C.seg_rows;
     return p;
 }
 
-bool nontemporal() { return env_int("WC_NT", 1) != 0; }
-int flat_tpw() { return env_int("WC_FLAT_TPW", 1); }
-
-int run(const Device &D, const wc::LaunchArgs &args, const Plan &p, hipStream_t st)
+int run(const Device &D, const Config &C, const wc::LaunchArgs &args, const Plan &p,
+        hipStream_t st)
 {
     (void)D;
     wc::LaunchArgs a = args;
     a.seg_rows = p.seg_rows;
-    a.grp_thr = env_int("WC_GRP_DENSE", 65) | (env_int("WC_GRP_SPARSE", 40) << 8);
-    a.grp_rows = env_int("WC_GRP_ROWS", 4);
+    a.grp_thr = C.grp_dense | (C.grp_sparse << 8);
+    a.grp_rows = C.grp_rows;
     hipError_t e = p.shape.group == 0 ? wc::launch_flat(a, p.shape.unroll, st)
                                       : wc::launch_cksum(a, p.shape, p.grid, st);
     return hip_err(e);
@@ -329,15 +393,17 @@ int batch_strided(const void *d_base, uint64_t stride, uint16_t len, uint64_t n,
     if (!d_base || (!d_out && !d_bad))
         return WC_EINVAL;
     Device *D = nullptr;
-    int rc = ensure_device(&D);
+    Config C;
+    int rc = ensure_device(&D, &C);
     if (rc)
         return rc;
-    const Plan p = plan_strided(*D, (uint64_t)d_base, stride, len, n, kind, d_out_hdr != nullptr);
+    const Plan p =
+        plan_strided(*D, C, (uint64_t)d_base, stride, len, n, kind, d_out_hdr != nullptr);
     wc::LaunchArgs a{d_base, stride, len,  nullptr,  nullptr, n,
-                     d_out,  d_bad,  kind, false,    p.full,  nontemporal(),
+                     d_out,  d_bad,  kind, false,    p.full,  C.nt != 0,
                      0,      d_out_hdr};
-    a.variant = env_int("WC_VARIANT", 0);
-    return run(*D, a, p, (hipStream_t)stream);
+    a.variant = C.variant;
+    return run(*D, C, a, p, (hipStream_t)stream);
 }
 
 int batch_ragged(const void *d_base, const uint64_t *d_off, const uint16_t *d_len,
@@ -351,15 +417,16 @@ int batch_ragged(const void *d_base, const uint64_t *d_off, const uint16_t *d_le
     if (!d_base || !d_off || !d_len || (!d_out && !d_bad))
         return WC_EINVAL;
     Device *D = nullptr;
-    int rc = ensure_device(&D);
+    Config C;
+    int rc = ensure_device(&D, &C);
     if (rc)
         return rc;
-    const Plan p = plan_ragged(*D, n, kind, false, d_out_hdr != nullptr);
+    const Plan p = plan_ragged(*D, C, n, kind, false, d_out_hdr != nullptr);
     wc::LaunchArgs a{d_base, 0,     0,    d_off, d_len, n,
-                     d_out,  d_bad, kind, true,  false, nontemporal(), flat_tpw(),
-                     d_out_hdr, env_int("WC_DIAG_NOLOAD", 0) != 0};
-    a.variant = env_int("WC_VARIANT", 0);
-    return run(*D, a, p, (hipStream_t)stream);
+                     d_out,  d_bad, kind, true,  false, C.nt != 0, C.flat_tpw,
+                     d_out_hdr, C.diag_noload != 0};
+    a.variant = C.variant;
+    return run(*D, C, a, p, (hipStream_t)stream);
 }
 
 [[noreturn]] void die(const char *what, int rc)
@@ -380,10 +447,10 @@ uint16_t scalar_cksum(const void *buf, uint16_t len, int kind, const char *who)
     const size_t span =
         kind == WC_CKSUM_PAYLOAD ? std::max<size_t>(len, 20) : (size_t)len;
     memcpy(D->h_stage, buf, span);
-    Plan p = plan_strided(*D, (uint64_t)D->d_stage, 0, len, 1, kind);
+    Plan p = plan_strided(*D, g_cfg, (uint64_t)D->d_stage, 0, len, 1, kind);
     wc::LaunchArgs a{D->d_stage, 0,   len,  nullptr, nullptr, 1,
                      D->d_res,   nullptr, kind, false,   p.full,  false};
-    rc = run(*D, a, p, D->scalar_st);
+    rc = run(*D, g_cfg, a, p, D->scalar_st);
     if (rc)
         die(who, rc);
     hipError_t e = hipStreamSynchronize(D->scalar_st);
@@ -458,8 +525,6 @@ uint64_t span_of(uint16_t len, int kind)
     return kind == WC_CKSUM_PAYLOAD ? std::max<uint64_t>(len, 20) : len;
 }
 
-int zc_bytes() { return env_int("WC_ZC_BYTES", kZcBytesDefault); }
-
 // Small registered batch: one launch reading host memory in place.
 int host_zero_copy(Device &D, const uint8_t *dbase, const uint64_t *h_off,
                    const uint16_t *h_len, uint64_t n, uint16_t *h_out, int kind)
@@ -470,11 +535,12 @@ int host_zero_copy(Device &D, const uint8_t *dbase, const uint64_t *h_off,
     ZeroCopy &Z = D.zc;
     memcpy(Z.h_off, h_off, n * 8);
     memcpy(Z.h_len, h_len, n * 2);
-    const Plan p = plan_ragged(D, n, kind, true);
+    const Config &C = g_cfg;
+    const Plan p = plan_ragged(D, C, n, kind, true);
     wc::LaunchArgs a{dbase, 0,       0,    Z.d_off, Z.d_len, n,
-                     Z.d_out, nullptr, kind, true,    false,   nontemporal(),
-                     flat_tpw()};
-    rc = run(D, a, p, Z.st);
+                     Z.d_out, nullptr, kind, true,    false,   C.nt != 0,
+                     C.flat_tpw};
+    rc = run(D, C, a, p, Z.st);
     if (rc)
         return rc;
     hipError_t e = hipStreamSynchronize(Z.st);
@@ -495,6 +561,14 @@ int host_pipeline(Device &D, const uint8_t *hb, bool registered, bool ascending,
     HostPipe &P = D.pipe;
     uint64_t pend_lo[kPipe] = {}, pend_n[kPipe] = {};
     bool pend[kPipe] = {};
+    // On any error, wait for every slot's in-flight copies and kernel before
+    // returning: they use the library's pinned staging, which the next call
+    // rewrites with plain memcpy.
+    auto fail = [&](int rc) -> int {
+        for (int s = 0; s < kPipe; ++s)
+            (void)hipStreamSynchronize(P.st[s]);
+        return rc;
+    };
     auto drain = [&](int s) -> int {
         if (!pend[s])
             return WC_OK;
@@ -511,7 +585,7 @@ int host_pipeline(Device &D, const uint8_t *hb, bool registered, bool ascending,
     while (i < n) {
         int rc = drain(slot);
         if (rc)
-            return rc;
+            return fail(rc);
         uint64_t j = i, bytes = 0;
         const uint8_t *src = nullptr;
         if (ascending) {
@@ -556,20 +630,21 @@ int host_pipeline(Device &D, const uint8_t *hb, bool registered, bool ascending,
             e = hipMemcpyAsync(P.d_len[slot], P.h_len[slot], cnt * 2,
                                hipMemcpyHostToDevice, st);
         if (e != hipSuccess)
-            return hip_err(e);
-        const Plan p = plan_ragged(D, cnt, kind);
+            return fail(hip_err(e));
+        const Config &C = g_cfg;
+        const Plan p = plan_ragged(D, C, cnt, kind);
         wc::LaunchArgs a{P.d_bytes[slot], 0,    0,    P.d_off[slot], P.d_len[slot],
                          cnt,             P.d_out[slot], nullptr, kind, true,
-                         false,           nontemporal(), flat_tpw()};
-        rc = run(D, a, p, st);
+                         false,           C.nt != 0,     C.flat_tpw};
+        rc = run(D, C, a, p, st);
         if (rc)
-            return rc;
+            return fail(rc);
         e = hipMemcpyAsync(P.h_out[slot], P.d_out[slot], cnt * 2,
                            hipMemcpyDeviceToHost, st);
         if (e == hipSuccess)
             e = hipEventRecord(P.done[slot], st);
         if (e != hipSuccess)
-            return hip_err(e);
+            return fail(hip_err(e));
         pend[slot] = true;
         pend_lo[slot] = i;
         pend_n[slot] = cnt;
@@ -579,7 +654,7 @@ int host_pipeline(Device &D, const uint8_t *hb, bool registered, bool ascending,
     for (int s = 0; s < kPipe; ++s) {
         int rc = drain((slot + s) % kPipe);
         if (rc)
-            return rc;
+            return fail(rc);
     }
     return WC_OK;
 }
@@ -718,7 +793,7 @@ int wc_cksum_host(const void *h_base, uint64_t h_bytes, const uint64_t *h_off,
     if (rc)
         return rc;
     const uint8_t *dbase = registered_dptr_locked(h_base, h_bytes);
-    if (dbase && n <= kZcPkts && total <= (uint64_t)zc_bytes())
+    if (dbase && n <= kZcPkts && total <= (uint64_t)g_cfg.zc_bytes)
         return host_zero_copy(*D, dbase, h_off, h_len, n, h_out, kind);
     rc = pipe_init_locked(*D);
     if (rc)
@@ -770,6 +845,20 @@ int wc_gpu_fini(void)
         (void)hipHostFree(D.h_res);
         D = Device{};
     }
+    // Drop the library's page-locks too: a later wc_gpu_init starts clean
+    // (a region still wanted must be registered again), and it re-reads the
+    // WC_* configuration.
+    for (auto &r : g_registered)
+        (void)hipHostUnregister((void *)r.first);
+    g_registered.clear();
+    g_cfg_loaded = false;
+    return WC_OK;
+}
+
+int wc_config_reload(void)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    load_config_locked();
     return WC_OK;
 }
 
@@ -780,7 +869,8 @@ int wc_synth_fill(void *d_buf, uint64_t nbytes, uint64_t seed, void *stream)
     if (!d_buf || ((uintptr_t)d_buf & 15u))
         return WC_EINVAL;
     Device *D = nullptr;
-    int rc = ensure_device(&D);
+    Config C;
+    int rc = ensure_device(&D, &C);
     if (rc)
         return rc;
     const uint64_t threads = (nbytes / 16) + 1;
@@ -796,10 +886,11 @@ int wc_plan_strided(uint64_t base_addr, uint64_t stride, uint16_t len,
     if (kind != WC_CKSUM_IP && kind != WC_CKSUM_PAYLOAD)
         return WC_EINVAL;
     Device *D = nullptr;
-    int rc = ensure_device(&D);
+    Config C;
+    int rc = ensure_device(&D, &C);
     if (rc)
         return rc;
-    const Plan p = plan_strided(*D, base_addr, stride, len, n, kind);
+    const Plan p = plan_strided(*D, C, base_addr, stride, len, n, kind);
     if (group)
         *group = p.shape.group;
     if (chunks_per_lane)

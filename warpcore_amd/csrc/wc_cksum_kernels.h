@@ -56,6 +56,11 @@
 
 namespace wc {
 
+// Largest grid any launcher uses: gridDim.x * 256 threads must fit in a
+// uint32 on AMD.  Every kernel strides over its work, so a capped grid stays
+// correct (wc_cksum_api.cpp grid_for, the ragged launchers).
+constexpr uint64_t kMaxGridBlocks = (1ull << 24) - 1;
+
 struct LaunchArgs {
     const void *base;
     uint64_t stride;

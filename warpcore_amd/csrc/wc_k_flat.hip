@@ -82,7 +82,8 @@ static hipError_t launch_flat_un(const LaunchArgs &a, hipStream_t st)
     const uint64_t tiles = (a.n + 63) / 64;
     const uint64_t tpw = (uint64_t)(a.tiles_per_wave > 0 ? a.tiles_per_wave : 1);
     const uint64_t waves = (tiles + tpw - 1) / tpw;
-    const int grid = (int)std::max<uint64_t>(1, (waves + kFlatWaves - 1) / kFlatWaves);
+    const int grid = (int)std::min<uint64_t>(
+        kMaxGridBlocks, std::max<uint64_t>(1, (waves + kFlatWaves - 1) / kFlatWaves));
     const uint8_t *b = (const uint8_t *)a.base;
     unsigned long long *bad = (unsigned long long *)a.bad;
 #define WC_FLAT(K, N, H)                                                       \

@@ -649,7 +649,8 @@ static hipError_t launch_seg_kernel(const LaunchArgs &a, hipStream_t st)
 {
     constexpr int UN = 2;
     const uint64_t tiles = (a.n + 63) / 64;
-    const int grid = (int)std::max<uint64_t>(1, (tiles + kFlatWaves - 1) / kFlatWaves);
+    const int grid = (int)std::min<uint64_t>(
+        kMaxGridBlocks, std::max<uint64_t>(1, (tiles + kFlatWaves - 1) / kFlatWaves));
     const uint8_t *b = (const uint8_t *)a.base;
     unsigned long long *bad = (unsigned long long *)a.bad;
     if (a.out_hdr) {
