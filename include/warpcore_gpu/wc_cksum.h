@@ -42,6 +42,7 @@ enum wc_cksum_kind {
 #define WC_EINVAL (-10001)   /* bad argument (NULL pointer, bad kind, ...) */
 #define WC_ENODEV (-10002)   /* no usable gfx950 device */
 #define WC_ENOMEM (-10003)   /* scratch / staging allocation failed */
+#define WC_ECOMM (-10004)    /* RCCL unavailable or a collective failed */
 
 /* --- drop-in scalar entry points (reference in_cksum.h:32-36) ------------ */
 
@@ -109,6 +110,59 @@ int wc_cksum_host(const void *h_base, uint64_t h_bytes, const uint64_t *h_off,
  * backend_netmap.c:149-151) so wc_cksum_host can DMA from it directly. */
 int wc_host_register(void *h_ptr, uint64_t bytes);
 int wc_host_unregister(void *h_ptr);
+
+/* --- multi-GPU batches (one host thread, G devices) ----------------------- */
+
+/* The batch shards across the GPUs of one node as an even contiguous split
+ * of packet indices: shard g of G holds packets
+ * [g*n/G, (g+1)*n/G).  Packets are independent, so no data moves between
+ * GPUs during the checksum; RCCL over xGMI is used only to gather the 2-byte
+ * results afterwards, if the caller wants them on every device.  Everything
+ * below is callable from warpcore's single engine thread (README.md:24-28). */
+
+/* Set up G shard executors, one per device: devices[g], or device g when
+ * `devices` is NULL (ngpus <= 0: every visible device).  A device may be
+ * listed more than once (shards then share it; rehearsal on fewer GPUs).
+ * Creates each device's scratch, streams and pinned staging.  The caller's
+ * current device is left unchanged. */
+int wc_gpu_init_multi(int ngpus, const int *devices);
+/* Number of shard executors set up by wc_gpu_init_multi (0 before). */
+int wc_gpu_multi_count(void);
+
+/* The even contiguous split: packets [*lo, *hi) of n go to shard g of G.
+ * Pure arithmetic (no GPU); the split every *_multi call uses. */
+int wc_shard_range(uint64_t n, int g, int ngpus, uint64_t *lo, uint64_t *hi);
+
+/* wc_cksum_host over the G shard devices: shard g's packets are copied to
+ * and checksummed on its own device (its own PCIe link and copy engines),
+ * the devices' pipelines interleaved by the calling thread; results land in
+ * h_out in packet order.  Synchronous.  A region registered with
+ * wc_host_register is DMA'd directly by every device.  A small registered
+ * batch (the zero-copy size of wc_cksum_host) runs on shard 0 alone.
+ * Before wc_gpu_init_multi this is wc_cksum_host on the current device. */
+int wc_cksum_host_multi(const void *h_base, uint64_t h_bytes, const uint64_t *h_off,
+                        const uint16_t *h_len, uint64_t n, uint16_t *h_out, int kind);
+
+/* Device-resident shards: shard g (g < wc_gpu_multi_count()) is the batch
+ * d_base[g] (+ d_off[g] / d_len[g]) of n[g] packets on shard g's device,
+ * results into d_out[g] on that device, enqueued on streams[g] (streams may
+ * be NULL: each device's default stream).  Asynchronous, like the
+ * single-device calls. */
+int wc_cksum_strided_multi(const void *const *d_base, uint64_t stride, uint16_t len,
+                           const uint64_t *n, uint16_t *const *d_out, int kind,
+                           void *const *streams);
+int wc_cksum_ragged_multi(const void *const *d_base, const uint64_t *const *d_off,
+                          const uint16_t *const *d_len, const uint64_t *n,
+                          uint16_t *const *d_out, int kind, void *const *streams);
+
+/* After the shards: every shard device g receives all Σn results in packet
+ * order in d_all[g] (shard h at offset Σ n[<h]) -- RCCL over xGMI, one
+ * ncclBroadcast per shard in one group, on communicators the library creates
+ * at the first call (ncclCommInitAll over the shard devices, which must be
+ * distinct) and frees in wc_gpu_fini.  Enqueued on streams[g]; RCCL is
+ * loaded at run time (WC_ECOMM if it is missing). */
+int wc_gather_results_multi(uint16_t *const *d_shard_out, const uint64_t *n,
+                            uint16_t *const *d_all, void *const *streams);
 
 /* --- library lifetime / introspection ------------------------------------ */
 

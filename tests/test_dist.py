@@ -80,3 +80,37 @@ def test_gloo_world2_sharded_equals_whole_batch(n):
         np.testing.assert_array_equal(got, whole)
         assert t == float(world)            # max over ranks
         assert bad == sum(range(world))     # sum over ranks
+
+
+def test_library_split_matches_for_1_to_8_gpus():
+    """wc_shard_range (the split the C host's *_multi calls use; pure
+    arithmetic, no GPU) equals the torch.distributed shard split, G = 1..8,
+    including uneven and 64-bit-sized batches."""
+    import warpcore_amd as wc
+    for n in (0, 1, 7, 1000, 1 << 20, (1 << 28) + 3, (1 << 62) + 5):
+        for w in range(1, 9):
+            got = [wc.shard_range(n, r, w) for r in range(w)]
+            assert got == [wdist.shard_range(n, r, w) for r in range(w)]
+            assert got[0][0] == 0 and got[-1][1] == n
+
+
+def test_library_split_rejects_bad_shard():
+    import warpcore_amd as wc
+    for g, w in ((2, 2), (-1, 2), (0, 0)):
+        with pytest.raises(wc.WcError):
+            wc.shard_range(10, g, w)
+
+
+def test_ragged_shards_cover_batch_in_order():
+    """Ragged shards (offsets/lengths split by packet count) rebased per
+    shard reproduce the whole batch in packet order."""
+    lens = synth.zipf_lengths(10007, seed=3)
+    offs = synth.packed_offsets(lens, lead=5)
+    for w in range(1, 9):
+        seen = []
+        for r in range(w):
+            o, l, first = wdist.shard_ragged(offs, lens, r, w)
+            assert first == wdist.shard_range(offs.size, r, w)[0]
+            seen.append((o, l))
+        np.testing.assert_array_equal(np.concatenate([o for o, _ in seen]), offs)
+        np.testing.assert_array_equal(np.concatenate([l for _, l in seen]), lens)

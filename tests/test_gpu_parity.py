@@ -579,6 +579,63 @@ def test_c_dropin_program(gpu, tmp_path):
     assert "dropin: ok" in r.stdout
 
 
+def test_c_multi_gpu_program(gpu, tmp_path):
+    """A single-threaded C host driving the multi-GPU ABI (tests/c/multi_test.c):
+    wc_cksum_host_multi over every visible GPU and over 4 shards sharing
+    cuda:0, device-resident shards and the RCCL result gather, all against
+    the oracle."""
+    exe = tmp_path / "multi_test"
+    subprocess.run(["gcc", "-O2", "-std=gnu11", "-D__HIP_PLATFORM_AMD__",
+                    "-I/opt/rocm/include", f"-I{ROOT / 'include'}", f"-I{ROOT / 'oracle'}",
+                    str(ROOT / "tests" / "c" / "multi_test.c"), str(ROOT / "oracle" / "wc_oracle.c"),
+                    "-o", str(exe), f"-L{ROOT / 'warpcore_amd'}", "-lwccksum",
+                    "-L/opt/rocm/lib", "-lamdhip64", "-lpthread",
+                    f"-Wl,-rpath,{ROOT / 'warpcore_amd'}"], check=True)
+    r = subprocess.run([str(exe), "300000"], capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "multi: ok" in r.stdout
+
+
+@pytest.mark.parametrize("kind", ["ip", "payload"])
+def test_host_multi_python(gpu, kind):
+    """The Python mirror of the multi-GPU host path: 3 shards sharing cuda:0,
+    wild IPv4/IPv6 packets, registered and pageable; then one shard per
+    visible GPU and the RCCL gather of device-resident shard results."""
+    rng = np.random.default_rng(31)
+    pkts = random_packets(rng, 60000, max_payload=1472, wild=True)
+    buf, offs, lens = pack(pkts, align=1, lead=7)
+    want = c_oracle.cksum_ragged(buf, offs, lens, kind=0 if kind == "ip" else 1)
+    try:
+        assert wc.gpu_init_multi(devices=[0, 0, 0]) == 3
+        np.testing.assert_array_equal(wc.cksum_host_multi(buf, offs, lens, kind=kind), want)
+        wc.host_register(buf)
+        try:
+            np.testing.assert_array_equal(wc.cksum_host_multi(buf, offs, lens, kind=kind), want)
+        finally:
+            wc.host_unregister(buf)
+        G = wc.gpu_init_multi()
+        devs = [torch.device("cuda", g) for g in range(G)]
+        bases, o_s, l_s, outs, counts = [], [], [], [], []
+        for g, dv in enumerate(devs):
+            lo, hi = wc.shard_range(lens.size, g, G)
+            b0 = int(offs[lo])
+            b1 = int(offs[hi - 1]) + max(int(lens[hi - 1]), 20)
+            bases.append(dev_u8(buf[b0:b1], dv))
+            o_s.append(to_dev((offs[lo:hi] - np.uint64(b0)).astype(np.uint64), dv))
+            l_s.append(to_dev(lens[lo:hi], dv))
+            outs.append(torch.empty(hi - lo, dtype=torch.uint16, device=dv))
+            counts.append(hi - lo)
+        wc.cksum_ragged_multi(bases, o_s, l_s, outs, kind=kind)
+        alls = [torch.empty(lens.size, dtype=torch.uint16, device=dv) for dv in devs]
+        wc.gather_results_multi(outs, counts, alls)
+        for a in alls:
+            torch.cuda.synchronize(a.device)
+            np.testing.assert_array_equal(host(a), want)
+    finally:
+        wc._lib.load().wc_gpu_fini()
+        wc.gpu_init(0)
+
+
 def build_sock_verify(out: Path) -> Path:
     subprocess.run(["gcc", "-O2", "-std=gnu11", "-D__HIP_PLATFORM_AMD__",
                     "-I/opt/rocm/include", f"-I{ROOT / 'include'}", f"-I{ROOT / 'oracle'}",

@@ -5,13 +5,17 @@ Product: ``libwccksum.so`` (HIP kernels + C ABI, ``include/warpcore_gpu``).
 This package is the Python host mirror of that C ABI plus the synthetic
 packet generators and the multi-GPU shard driver used by bench.py.
 """
-from .cksum import (KIND_IP, KIND_PAYLOAD, WcError, cksum_host, cksum_ip_udp_ragged,
+from .cksum import (KIND_IP, KIND_PAYLOAD, WcError, cksum_host, cksum_host_multi,
+                    cksum_ip_udp_ragged, cksum_ragged_multi, gather_results_multi,
+                    gpu_init_multi, shard_range,
                     cksum_ip_udp_strided, cksum_ragged, cksum_strided, gpu_init, host_register, host_unregister,
                     ip_cksum, payload_cksum, plan_strided, reload_config, synth_fill,
                     verify_ragged, verify_strided, version)
 
 __all__ = [
-    "KIND_IP", "KIND_PAYLOAD", "WcError", "cksum_host", "cksum_ip_udp_ragged",
+    "KIND_IP", "KIND_PAYLOAD", "WcError", "cksum_host", "cksum_host_multi",
+    "cksum_ip_udp_ragged", "cksum_ragged_multi", "gather_results_multi", "gpu_init_multi",
+    "shard_range",
     "cksum_ip_udp_strided", "cksum_ragged",
     "cksum_strided", "gpu_init", "host_register", "host_unregister", "ip_cksum",
     "payload_cksum", "plan_strided", "reload_config", "synth_fill", "verify_ragged",

@@ -24,9 +24,9 @@ INCLUDE = ROOT / "include"
 LIB = PKG / "libwccksum.so"
 ORACLE_DIR = ROOT / "oracle"
 
-HIP_SOURCES = [CSRC / "wc_k_strided.hip", CSRC / "wc_k_seg.hip", CSRC / "wc_k_flat.hip",
+HIP_SOURCES = [CSRC / "wc_k_strided.hip", CSRC / "wc_k_seg.hip", CSRC / "wc_k_flat.hip", CSRC / "wc_rccl.cpp",
                CSRC / "wc_k_synth.hip", CSRC / "wc_cksum_api.cpp"]
-HIP_DEPS = HIP_SOURCES + [CSRC / "wc_cksum_kernels.h", CSRC / "wc_device.h", CSRC / "wc_flat.h",
+HIP_DEPS = HIP_SOURCES + [CSRC / "wc_cksum_kernels.h", CSRC / "wc_rccl.h", CSRC / "wc_device.h", CSRC / "wc_flat.h",
                           INCLUDE / "warpcore_gpu" / "wc_cksum.h"]
 ORACLE_SOURCES = [ORACLE_DIR / "wc_oracle.c", ORACLE_DIR / "wc_oracle.h"]
 

@@ -36,6 +36,13 @@ SIGNATURES = {
     "wc_host_register": (_int, [_vp, _u64]),
     "wc_host_unregister": (_int, [_vp]),
     "wc_gpu_init": (_int, [_int]),
+    "wc_gpu_init_multi": (_int, [_int, _vp]),
+    "wc_gpu_multi_count": (_int, []),
+    "wc_shard_range": (_int, [_u64, _int, _int, ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
+    "wc_cksum_host_multi": (_int, [_vp, _u64, _vp, _vp, _u64, _vp, _int]),
+    "wc_cksum_strided_multi": (_int, [_vp, _u64, _u16, _vp, _vp, _int, _vp]),
+    "wc_cksum_ragged_multi": (_int, [_vp, _vp, _vp, _vp, _vp, _int, _vp]),
+    "wc_gather_results_multi": (_int, [_vp, _vp, _vp, _vp]),
     "wc_gpu_fini": (_int, []),
     "wc_config_reload": (_int, []),
     "wc_synth_fill": (_int, [_vp, _u64, _u64, _vp]),

@@ -363,3 +363,75 @@ def gpu_init(device: int = -1) -> None:
 
 def version() -> str:
     return _lib.load().wc_version().decode()
+
+
+# --------------------------------------------------------------------------
+# Multi-GPU from one host thread (the C host's path).
+
+def shard_range(n: int, g: int, ngpus: int) -> Tuple[int, int]:
+    """The library's even contiguous split: packets [lo, hi) of n for shard g."""
+    lo, hi = ctypes.c_uint64(), ctypes.c_uint64()
+    _check("wc_shard_range", _lib.load().wc_shard_range(n, g, ngpus, ctypes.byref(lo),
+                                                        ctypes.byref(hi)))
+    return lo.value, hi.value
+
+
+def gpu_init_multi(ngpus: int = 0, devices=None) -> int:
+    """Set up one shard executor per device (devices[g], or g); returns G."""
+    arr = None
+    if devices is not None:
+        devices = list(devices)
+        ngpus = len(devices)
+        arr = (ctypes.c_int * ngpus)(*devices)
+    _check("wc_gpu_init_multi", _lib.load().wc_gpu_init_multi(ngpus, arr))
+    return int(_lib.load().wc_gpu_multi_count())
+
+
+def cksum_host_multi(buf: np.ndarray, offsets: np.ndarray, lengths: np.ndarray,
+                     kind="ip") -> np.ndarray:
+    """cksum_host split evenly over the shard devices (wc_cksum_host_multi)."""
+    buf = np.ascontiguousarray(buf).reshape(-1).view(np.uint8)
+    lens_in = np.asarray(lengths)
+    if lens_in.size and (lens_in.min() < 0 or lens_in.max() > 0xFFFF):
+        raise ValueError("len is a uint16 in the reference (0..65535)")
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens_in, dtype=np.uint16)
+    if off.shape != lens.shape:
+        raise ValueError("offsets and lengths must have the same shape")
+    out = np.empty(off.size, dtype=np.uint16)
+    _check("wc_cksum_host_multi", _lib.load().wc_cksum_host_multi(
+        buf.ctypes.data, buf.size, off.ctypes.data, lens.ctypes.data, off.size,
+        out.ctypes.data, _kind(kind)))
+    return out
+
+
+def _ptrs(ts) -> ctypes.Array:
+    return (ctypes.c_void_p * len(ts))(*[t.data_ptr() if isinstance(t, torch.Tensor) else t
+                                         for t in ts])
+
+
+def cksum_ragged_multi(bases, offsets, lengths, outs, kind="ip", streams=None) -> None:
+    """Shard g's device-resident batch (bases[g], offsets[g], lengths[g]) into
+    outs[g], each on shard g's device (asynchronous)."""
+    k = _kind(kind)
+    G = len(bases)
+    for b, o, l, r in zip(bases, offsets, lengths, outs):
+        n = _check_ragged(b, o, l, k, True)
+        _out_tensor(r, n, b.device)
+    ns = (ctypes.c_uint64 * G)(*[o.numel() for o in offsets])
+    st = None if streams is None else _ptrs([_stream_ptr(s) for s in streams])
+    _check("wc_cksum_ragged_multi", _lib.load().wc_cksum_ragged_multi(
+        _ptrs(bases), _ptrs(offsets), _ptrs(lengths), ns, _ptrs(outs), k, st))
+
+
+def gather_results_multi(shard_outs, counts, all_outs, streams=None) -> None:
+    """RCCL all-gather of every shard's results into all_outs[g] (packet order)."""
+    G = len(shard_outs)
+    total = sum(int(c) for c in counts)
+    for a in all_outs:
+        if a.numel() < total or a.element_size() != 2:
+            raise ValueError("each all_outs tensor needs sum(counts) 2-byte entries")
+    ns = (ctypes.c_uint64 * G)(*[int(c) for c in counts])
+    st = None if streams is None else _ptrs([_stream_ptr(s) for s in streams])
+    _check("wc_gather_results_multi", _lib.load().wc_gather_results_multi(
+        _ptrs(shard_outs), ns, _ptrs(all_outs), st))

@@ -11,6 +11,7 @@
 #include "warpcore_gpu/wc_cksum.h"
 
 #include "wc_cksum_kernels.h"
+#include "wc_rccl.h"
 
 #include <hip/hip_runtime.h>
 
@@ -116,6 +117,15 @@ Device g_dev[kMaxDevices];
 std::map<uintptr_t, Registration> g_registered; // host base -> region
 Config g_cfg;
 bool g_cfg_loaded = false;
+
+// Multi-GPU shard executors (wc_gpu_init_multi): shard g runs on device
+// g_shard[g].dev with its own host pipeline, so two shards may share a GPU.
+struct ShardExec {
+    int dev = -1;
+    HostPipe pipe;
+};
+ShardExec g_shard[kMaxDevices];
+int g_multi_n = 0;
 
 int hip_err(hipError_t e) { return e == hipSuccess ? WC_OK : -(int)e; }
 
@@ -462,9 +472,10 @@ uint16_t scalar_cksum(const void *buf, uint16_t len, int kind, const char *who)
 // ---------------------------------------------------------------------------
 // Host-memory pipeline.
 
-int pipe_init_locked(Device &D)
+// Streams, events and staging of one host pipeline, created on the current
+// device.
+int pipe_init_locked(HostPipe &P)
 {
-    HostPipe &P = D.pipe;
     if (P.ready)
         return WC_OK;
     for (int s = 0; s < kPipe; ++s) {
@@ -484,6 +495,26 @@ int pipe_init_locked(Device &D)
     }
     P.ready = true;
     return WC_OK;
+}
+
+void pipe_free(HostPipe &P)
+{
+    if (!P.ready)
+        return;
+    for (int s = 0; s < kPipe; ++s) {
+        (void)hipStreamSynchronize(P.st[s]);
+        (void)hipFree(P.d_bytes[s]);
+        (void)hipFree(P.d_off[s]);
+        (void)hipFree(P.d_len[s]);
+        (void)hipFree(P.d_out[s]);
+        (void)hipHostFree(P.h_bytes[s]);
+        (void)hipHostFree(P.h_off[s]);
+        (void)hipHostFree(P.h_len[s]);
+        (void)hipHostFree(P.h_out[s]);
+        (void)hipEventDestroy(P.done[s]);
+        (void)hipStreamDestroy(P.st[s]);
+    }
+    P = HostPipe{};
 }
 
 int zc_init_locked(Device &D)
@@ -554,109 +585,214 @@ int host_zero_copy(Device &D, const uint8_t *dbase, const uint64_t *h_off,
 // H2D -> kernel -> D2H.  An ascending batch ships the byte range its chunk
 // covers (straight from registered memory, else via pinned staging); any
 // other order is gathered packet by packet into pinned staging first.
-int host_pipeline(Device &D, const uint8_t *hb, bool registered, bool ascending,
-                  const uint64_t *h_off, const uint16_t *h_len, uint64_t n,
-                  uint16_t *h_out, int kind)
-{
-    HostPipe &P = D.pipe;
+//
+// A PipeRun walks packets [i, hi) of a batch through one HostPipe on one
+// device, one chunk per step(), so a single host thread can interleave the
+// runs of several devices (wc_cksum_host_multi): while it stages device g's
+// next chunk, the other devices' copies and kernels are in flight.
+struct PipeRun {
+    Device *D = nullptr;
+    HostPipe *P = nullptr;
+    int dev = 0;
+    const uint8_t *hb = nullptr;
+    bool registered = false, ascending = true;
+    const uint64_t *h_off = nullptr;
+    const uint16_t *h_len = nullptr;
+    uint16_t *h_out = nullptr;
+    int kind = WC_CKSUM_IP;
+    uint64_t i = 0, hi = 0;
     uint64_t pend_lo[kPipe] = {}, pend_n[kPipe] = {};
     bool pend[kPipe] = {};
+    int slot = 0;
+
+    bool done() const { return i >= hi; }
+
+    // Wait for a slot's chunk and copy its results out.
+    int drain(int s)
+    {
+        if (!pend[s])
+            return WC_OK;
+        hipError_t e = hipEventSynchronize(P->done[s]);
+        if (e != hipSuccess)
+            return hip_err(e);
+        memcpy(h_out + pend_lo[s], P->h_out[s], pend_n[s] * 2);
+        pend[s] = false;
+        return WC_OK;
+    }
+
     // On any error, wait for every slot's in-flight copies and kernel before
     // returning: they use the library's pinned staging, which the next call
     // rewrites with plain memcpy.
-    auto fail = [&](int rc) -> int {
-        for (int s = 0; s < kPipe; ++s)
-            (void)hipStreamSynchronize(P.st[s]);
+    int fail(int rc)
+    {
+        for (int s = 0; s < kPipe; ++s) {
+            (void)hipStreamSynchronize(P->st[s]);
+            pend[s] = false;
+        }
         return rc;
-    };
-    auto drain = [&](int s) -> int {
-        if (!pend[s])
-            return WC_OK;
-        hipError_t e = hipEventSynchronize(P.done[s]);
-        if (e != hipSuccess)
-            return hip_err(e);
-        memcpy(h_out + pend_lo[s], P.h_out[s], pend_n[s] * 2);
-        pend[s] = false;
-        return WC_OK;
-    };
+    }
 
-    uint64_t i = 0;
-    int slot = 0;
-    while (i < n) {
+    // Stage and enqueue the next chunk (caller: current device = dev).
+    int step()
+    {
         int rc = drain(slot);
         if (rc)
-            return fail(rc);
+            return rc;
+        const uint64_t i0 = i;
         uint64_t j = i, bytes = 0;
         const uint8_t *src = nullptr;
         if (ascending) {
             const uint64_t lo = h_off[i];
-            uint64_t hi = lo;
-            while (j < n && j - i < kChunkPkts) {
+            uint64_t top = lo;
+            while (j < hi && j - i0 < kChunkPkts) {
                 const uint64_t e = h_off[j] + span_of(h_len[j], kind);
-                if (std::max(hi, e) - lo > kChunkBytes && j > i)
+                if (std::max(top, e) - lo > kChunkBytes && j > i0)
                     break;
-                hi = std::max(hi, e);
-                P.h_off[slot][j - i] = h_off[j] - lo;
-                P.h_len[slot][j - i] = h_len[j];
+                top = std::max(top, e);
+                P->h_off[slot][j - i0] = h_off[j] - lo;
+                P->h_len[slot][j - i0] = h_len[j];
                 ++j;
             }
-            bytes = hi - lo;
+            bytes = top - lo;
             src = hb + lo;
             if (!registered) {
-                memcpy(P.h_bytes[slot], src, bytes);
-                src = P.h_bytes[slot];
+                memcpy(P->h_bytes[slot], src, bytes);
+                src = P->h_bytes[slot];
             }
         } else {
-            while (j < n && j - i < kChunkPkts) {
+            while (j < hi && j - i0 < kChunkPkts) {
                 const uint64_t sp = span_of(h_len[j], kind);
-                if (bytes + sp > kChunkBytes && j > i)
+                if (bytes + sp > kChunkBytes && j > i0)
                     break;
-                memcpy(P.h_bytes[slot] + bytes, hb + h_off[j], sp);
-                P.h_off[slot][j - i] = bytes;
-                P.h_len[slot][j - i] = h_len[j];
+                memcpy(P->h_bytes[slot] + bytes, hb + h_off[j], sp);
+                P->h_off[slot][j - i0] = bytes;
+                P->h_len[slot][j - i0] = h_len[j];
                 bytes += sp;
                 ++j;
             }
-            src = P.h_bytes[slot];
+            src = P->h_bytes[slot];
         }
-        const uint64_t cnt = j - i;
-        hipStream_t st = P.st[slot];
-        hipError_t e = hipMemcpyAsync(P.d_bytes[slot], src, bytes,
-                                      hipMemcpyHostToDevice, st);
+        const uint64_t cnt = j - i0;
+        hipStream_t st = P->st[slot];
+        hipError_t e = hipMemcpyAsync(P->d_bytes[slot], src, bytes, hipMemcpyHostToDevice, st);
         if (e == hipSuccess)
-            e = hipMemcpyAsync(P.d_off[slot], P.h_off[slot], cnt * 8,
-                               hipMemcpyHostToDevice, st);
+            e = hipMemcpyAsync(P->d_off[slot], P->h_off[slot], cnt * 8, hipMemcpyHostToDevice,
+                               st);
         if (e == hipSuccess)
-            e = hipMemcpyAsync(P.d_len[slot], P.h_len[slot], cnt * 2,
-                               hipMemcpyHostToDevice, st);
+            e = hipMemcpyAsync(P->d_len[slot], P->h_len[slot], cnt * 2, hipMemcpyHostToDevice,
+                               st);
         if (e != hipSuccess)
-            return fail(hip_err(e));
+            return hip_err(e);
         const Config &C = g_cfg;
-        const Plan p = plan_ragged(D, C, cnt, kind);
-        wc::LaunchArgs a{P.d_bytes[slot], 0,    0,    P.d_off[slot], P.d_len[slot],
-                         cnt,             P.d_out[slot], nullptr, kind, true,
-                         false,           C.nt != 0,     C.flat_tpw};
-        rc = run(D, C, a, p, st);
+        const Plan p = plan_ragged(*D, C, cnt, kind);
+        wc::LaunchArgs a{P->d_bytes[slot], 0,    0,    P->d_off[slot], P->d_len[slot],
+                         cnt,              P->d_out[slot], nullptr, kind, true,
+                         false,            C.nt != 0,      C.flat_tpw};
+        rc = run(*D, C, a, p, st);
         if (rc)
-            return fail(rc);
-        e = hipMemcpyAsync(P.h_out[slot], P.d_out[slot], cnt * 2,
-                           hipMemcpyDeviceToHost, st);
+            return rc;
+        e = hipMemcpyAsync(P->h_out[slot], P->d_out[slot], cnt * 2, hipMemcpyDeviceToHost, st);
         if (e == hipSuccess)
-            e = hipEventRecord(P.done[slot], st);
+            e = hipEventRecord(P->done[slot], st);
         if (e != hipSuccess)
-            return fail(hip_err(e));
+            return hip_err(e);
         pend[slot] = true;
-        pend_lo[slot] = i;
+        pend_lo[slot] = i0;
         pend_n[slot] = cnt;
         i = j;
         slot = (slot + 1) % kPipe;
+        return WC_OK;
     }
-    for (int s = 0; s < kPipe; ++s) {
-        int rc = drain((slot + s) % kPipe);
+
+    int finish()
+    {
+        for (int s = 0; s < kPipe; ++s) {
+            int rc = drain((slot + s) % kPipe);
+            if (rc)
+                return rc;
+        }
+        return WC_OK;
+    }
+};
+
+// Every packet of a host batch inside [0, h_bytes); its order and bytes.
+bool host_batch_ok(uint64_t h_bytes, const uint64_t *h_off, const uint16_t *h_len, uint64_t n,
+                   int kind, bool *ascending, uint64_t *total)
+{
+    bool asc = true;
+    uint64_t tot = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t o = h_off[i];
+        const uint64_t sp = span_of(h_len[i], kind);
+        if (o > h_bytes || sp > h_bytes - o)
+            return false;
+        asc &= i == 0 || o >= h_off[i - 1];
+        tot += sp;
+    }
+    *ascending = asc;
+    *total = tot;
+    return true;
+}
+
+void shard_range(uint64_t n, int g, int G, uint64_t *lo, uint64_t *hi)
+{
+    // n * g / G without overflow for any uint64 n
+    *lo = (uint64_t)((unsigned __int128)n * (unsigned)g / (unsigned)G);
+    *hi = (uint64_t)((unsigned __int128)n * (unsigned)(g + 1) / (unsigned)G);
+}
+
+int host_pipeline(Device &D, const uint8_t *hb, bool registered, bool ascending,
+                  const uint64_t *h_off, const uint16_t *h_len, uint64_t n,
+                  uint16_t *h_out, int kind)
+{
+    PipeRun r;
+    r.D = &D;
+    r.P = &D.pipe;
+    r.hb = hb;
+    r.registered = registered;
+    r.ascending = ascending;
+    r.h_off = h_off;
+    r.h_len = h_len;
+    r.h_out = h_out;
+    r.kind = kind;
+    r.hi = n;
+    while (!r.done()) {
+        const int rc = r.step();
         if (rc)
-            return fail(rc);
+            return r.fail(rc);
     }
-    return WC_OK;
+    const int rc = r.finish();
+    return rc ? r.fail(rc) : WC_OK;
+}
+
+
+// Run fn(g) for every shard with its device current; the caller's device is
+// restored.  Snapshot of the shard devices taken under the lock (the batch
+// calls take it themselves).
+template <class F>
+int for_each_shard(F &&fn)
+{
+    int devs[kMaxDevices];
+    int G = 0;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        G = g_multi_n;
+        for (int g = 0; g < G; ++g)
+            devs[g] = g_shard[g].dev;
+    }
+    if (G == 0)
+        return WC_EINVAL; // wc_gpu_init_multi first
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess)
+        return WC_ENODEV;
+    int rc = WC_OK;
+    for (int g = 0; g < G && rc == WC_OK; ++g) {
+        rc = hip_err(hipSetDevice(devs[g]));
+        if (rc == WC_OK)
+            rc = fn(g);
+    }
+    (void)hipSetDevice(cur);
+    return rc;
 }
 
 } // namespace
@@ -740,7 +876,8 @@ int wc_host_register(void *h_ptr, uint64_t bytes)
     int rc = init_locked(-1, &D);
     if (rc)
         return rc;
-    hipError_t e = hipHostRegister(h_ptr, bytes, hipHostRegisterMapped);
+    // Portable: every device (wc_cksum_host_multi's shards) may DMA from it.
+    hipError_t e = hipHostRegister(h_ptr, bytes, hipHostRegisterMapped | hipHostRegisterPortable);
     if (e != hipSuccess)
         return hip_err(e);
     void *dptr = nullptr;
@@ -774,18 +911,10 @@ int wc_cksum_host(const void *h_base, uint64_t h_bytes, const uint64_t *h_off,
         return WC_OK;
     if (!h_base || !h_off || !h_len || !h_out)
         return WC_EINVAL;
-
-    // Every packet must lie inside the region; note the order and the bytes.
     bool ascending = true;
     uint64_t total = 0;
-    for (uint64_t i = 0; i < n; ++i) {
-        const uint64_t o = h_off[i];
-        const uint64_t sp = span_of(h_len[i], kind);
-        if (o > h_bytes || sp > h_bytes - o)
-            return WC_EINVAL;
-        ascending &= i == 0 || o >= h_off[i - 1];
-        total += sp;
-    }
+    if (!host_batch_ok(h_bytes, h_off, h_len, n, kind, &ascending, &total))
+        return WC_EINVAL;
 
     std::lock_guard<std::mutex> lk(g_mu);
     Device *D = nullptr;
@@ -795,11 +924,197 @@ int wc_cksum_host(const void *h_base, uint64_t h_bytes, const uint64_t *h_off,
     const uint8_t *dbase = registered_dptr_locked(h_base, h_bytes);
     if (dbase && n <= kZcPkts && total <= (uint64_t)g_cfg.zc_bytes)
         return host_zero_copy(*D, dbase, h_off, h_len, n, h_out, kind);
-    rc = pipe_init_locked(*D);
+    rc = pipe_init_locked(D->pipe);
     if (rc)
         return rc;
     return host_pipeline(*D, (const uint8_t *)h_base, dbase != nullptr, ascending,
                          h_off, h_len, n, h_out, kind);
+}
+
+// ---------------------------------------------------------------------------
+// Multi-GPU: an even contiguous packet split over the shard
+// executors, no data-path collective; RCCL only for the optional result
+// gather.
+
+int wc_shard_range(uint64_t n, int g, int ngpus, uint64_t *lo, uint64_t *hi)
+{
+    if (ngpus < 1 || g < 0 || g >= ngpus || !lo || !hi)
+        return WC_EINVAL;
+    shard_range(n, g, ngpus, lo, hi);
+    return WC_OK;
+}
+
+int wc_gpu_init_multi(int ngpus, const int *devices)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return WC_ENODEV;
+    if (ngpus <= 0) {
+        if (devices)
+            return WC_EINVAL;
+        ngpus = ndev;
+    }
+    if (ngpus > kMaxDevices)
+        return WC_EINVAL;
+    int devs[kMaxDevices];
+    for (int g = 0; g < ngpus; ++g) {
+        devs[g] = devices ? devices[g] : g;
+        if (devs[g] < 0 || devs[g] >= ndev || devs[g] >= kMaxDevices)
+            return WC_EINVAL;
+    }
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess)
+        return WC_ENODEV;
+    // A new shard set replaces the old one (its pipelines and communicators).
+    wc::rccl_fini();
+    for (int g = 0; g < g_multi_n; ++g) {
+        (void)hipSetDevice(g_shard[g].dev);
+        pipe_free(g_shard[g].pipe);
+        g_shard[g] = ShardExec{};
+    }
+    g_multi_n = 0;
+    int rc = WC_OK;
+    for (int g = 0; g < ngpus && rc == WC_OK; ++g) {
+        Device *D = nullptr;
+        rc = init_locked(devs[g], &D); // sets device devs[g]
+        if (rc == WC_OK)
+            rc = pipe_init_locked(g_shard[g].pipe);
+        g_shard[g].dev = devs[g];
+        g_multi_n = g + 1;
+    }
+    (void)hipSetDevice(cur);
+    return rc;
+}
+
+int wc_gpu_multi_count(void)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    return g_multi_n;
+}
+
+int wc_cksum_host_multi(const void *h_base, uint64_t h_bytes, const uint64_t *h_off,
+                        const uint16_t *h_len, uint64_t n, uint16_t *h_out, int kind)
+{
+    if (kind != WC_CKSUM_IP && kind != WC_CKSUM_PAYLOAD)
+        return WC_EINVAL;
+    if (n == 0)
+        return WC_OK;
+    if (!h_base || !h_off || !h_len || !h_out)
+        return WC_EINVAL;
+    int G = 0;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        G = g_multi_n;
+    }
+    if (G == 0)
+        return wc_cksum_host(h_base, h_bytes, h_off, h_len, n, h_out, kind);
+    bool ascending = true;
+    uint64_t total = 0;
+    if (!host_batch_ok(h_bytes, h_off, h_len, n, kind, &ascending, &total))
+        return WC_EINVAL;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        G = g_multi_n;
+        int cur = 0;
+        if (hipGetDevice(&cur) != hipSuccess)
+            return WC_ENODEV;
+        const uint8_t *dbase = registered_dptr_locked(h_base, h_bytes);
+        if (dbase && n <= kZcPkts && total <= (uint64_t)g_cfg.zc_bytes) {
+            // Small registered batch: one zero-copy launch on shard 0.
+            Device *D = nullptr;
+            int rc = init_locked(g_shard[0].dev, &D);
+            if (rc == WC_OK)
+                rc = host_zero_copy(*D, dbase, h_off, h_len, n, h_out, kind);
+            (void)hipSetDevice(cur);
+            return rc;
+        }
+        PipeRun runs[kMaxDevices];
+        for (int g = 0; g < G; ++g) {
+            PipeRun &r = runs[g];
+            r.D = &g_dev[g_shard[g].dev];
+            r.P = &g_shard[g].pipe;
+            r.dev = g_shard[g].dev;
+            r.hb = (const uint8_t *)h_base;
+            r.registered = dbase != nullptr;
+            r.ascending = ascending;
+            r.h_off = h_off;
+            r.h_len = h_len;
+            r.h_out = h_out;
+            r.kind = kind;
+            shard_range(n, g, G, &r.i, &r.hi);
+        }
+        // One thread, G pipelines: each pass stages one chunk per unfinished
+        // shard, so every device's copies and kernels overlap the staging of
+        // the others.
+        int rc = WC_OK;
+        for (bool more = true; more && rc == WC_OK;) {
+            more = false;
+            for (int g = 0; g < G && rc == WC_OK; ++g) {
+                if (runs[g].done())
+                    continue;
+                more = true;
+                rc = hip_err(hipSetDevice(runs[g].dev));
+                if (rc == WC_OK)
+                    rc = runs[g].step();
+            }
+        }
+        for (int g = 0; g < G; ++g) {
+            (void)hipSetDevice(runs[g].dev);
+            if (rc == WC_OK)
+                rc = runs[g].finish();
+        }
+        if (rc != WC_OK)
+            for (int g = 0; g < G; ++g) {
+                (void)hipSetDevice(runs[g].dev);
+                (void)runs[g].fail(rc);
+            }
+        (void)hipSetDevice(cur);
+        return rc;
+    }
+}
+
+int wc_cksum_strided_multi(const void *const *d_base, uint64_t stride, uint16_t len,
+                           const uint64_t *n, uint16_t *const *d_out, int kind,
+                           void *const *streams)
+{
+    if (!d_base || !n || !d_out)
+        return WC_EINVAL;
+    return for_each_shard([&](int g) {
+        return wc_cksum_strided(d_base[g], stride, len, n[g], d_out[g], kind,
+                                streams ? streams[g] : nullptr);
+    });
+}
+
+int wc_cksum_ragged_multi(const void *const *d_base, const uint64_t *const *d_off,
+                          const uint16_t *const *d_len, const uint64_t *n,
+                          uint16_t *const *d_out, int kind, void *const *streams)
+{
+    if (!d_base || !d_off || !d_len || !n || !d_out)
+        return WC_EINVAL;
+    return for_each_shard([&](int g) {
+        return wc_cksum_ragged(d_base[g], d_off[g], d_len[g], n[g], d_out[g], kind,
+                               streams ? streams[g] : nullptr);
+    });
+}
+
+int wc_gather_results_multi(uint16_t *const *d_shard_out, const uint64_t *n,
+                            uint16_t *const *d_all, void *const *streams)
+{
+    if (!d_shard_out || !n || !d_all)
+        return WC_EINVAL;
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_multi_n == 0)
+        return WC_EINVAL;
+    int devs[kMaxDevices];
+    for (int g = 0; g < g_multi_n; ++g)
+        devs[g] = g_shard[g].dev;
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess)
+        return WC_ENODEV;
+    const int rc = wc::rccl_allgatherv_u16(g_multi_n, devs, d_shard_out, n, d_all, streams);
+    (void)hipSetDevice(cur);
+    return rc;
 }
 
 int wc_gpu_init(int device)
@@ -812,26 +1127,21 @@ int wc_gpu_init(int device)
 int wc_gpu_fini(void)
 {
     std::lock_guard<std::mutex> lk(g_mu);
-    for (auto &D : g_dev) {
+    int cur = 0;
+    const bool have_cur = hipGetDevice(&cur) == hipSuccess;
+    wc::rccl_fini();
+    for (int g = 0; g < g_multi_n; ++g) {
+        (void)hipSetDevice(g_shard[g].dev);
+        pipe_free(g_shard[g].pipe);
+        g_shard[g] = ShardExec{};
+    }
+    g_multi_n = 0;
+    for (int d = 0; d < kMaxDevices; ++d) {
+        Device &D = g_dev[d];
         if (!D.ok)
             continue;
-        HostPipe &P = D.pipe;
-        if (P.ready) {
-            for (int s = 0; s < kPipe; ++s) {
-                (void)hipStreamSynchronize(P.st[s]);
-                (void)hipFree(P.d_bytes[s]);
-                (void)hipFree(P.d_off[s]);
-                (void)hipFree(P.d_len[s]);
-                (void)hipFree(P.d_out[s]);
-                (void)hipHostFree(P.h_bytes[s]);
-                (void)hipHostFree(P.h_off[s]);
-                (void)hipHostFree(P.h_len[s]);
-                (void)hipHostFree(P.h_out[s]);
-                (void)hipEventDestroy(P.done[s]);
-                (void)hipStreamDestroy(P.st[s]);
-            }
-            P = HostPipe{};
-        }
+        (void)hipSetDevice(d);
+        pipe_free(D.pipe);
         if (D.zc.ready) {
             (void)hipStreamSynchronize(D.zc.st);
             (void)hipStreamDestroy(D.zc.st);
@@ -852,6 +1162,8 @@ int wc_gpu_fini(void)
         (void)hipHostUnregister((void *)r.first);
     g_registered.clear();
     g_cfg_loaded = false;
+    if (have_cur)
+        (void)hipSetDevice(cur);
     return WC_OK;
 }
 
@@ -913,6 +1225,8 @@ const char *wc_strerror(int err)
         return "no usable gfx950 device";
     case WC_ENOMEM:
         return "out of memory";
+    case WC_ECOMM:
+        return "RCCL unavailable or collective failed";
     default:
         if (err < 0 && err > -10000)
             return hipGetErrorString((hipError_t)(-err));
