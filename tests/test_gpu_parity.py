@@ -44,6 +44,7 @@ def host(t: torch.Tensor) -> np.ndarray:
 # forced for every tile; and the default per-tile choice.
 RAGGED_MODES = {
     "flat": {"WC_SEG": "0"},
+    "flat2": {"WC_SEG": "0", "WC_FLAT_PK": "2"},
     "seg": {"WC_SEG": "1", "WC_GRP_DENSE": "65", "WC_GRP_SPARSE": "65"},
     "grp": {"WC_SEG": "1", "WC_GRP_DENSE": "0", "WC_GRP_SPARSE": "0"},
     "default": {},
@@ -51,7 +52,7 @@ RAGGED_MODES = {
 
 
 def ragged_mode(monkeypatch, mode: str) -> None:
-    for k in ("WC_SEG", "WC_GRP_DENSE", "WC_GRP_SPARSE"):
+    for k in ("WC_SEG", "WC_GRP_DENSE", "WC_GRP_SPARSE", "WC_FLAT_PK"):
         monkeypatch.delenv(k, raising=False)
     for k, v in RAGGED_MODES[mode].items():
         monkeypatch.setenv(k, v)
@@ -469,7 +470,7 @@ def test_c3_mtu_sweep_full(gpu, L):
     np.testing.assert_array_equal(got, c_oracle.cksum_strided(hb, L, L, n, kind=0))
 
 
-@pytest.mark.parametrize("mode", ["default", "flat"])
+@pytest.mark.parametrize("mode", ["default", "flat", "flat2"])
 def test_c4_zipf_full(gpu, monkeypatch, mode):
     """C4 in full through the seg kernel (default) and the flat kernel."""
     ragged_mode(monkeypatch, mode)
@@ -480,6 +481,45 @@ def test_c4_zipf_full(gpu, monkeypatch, mode):
     got = host(wc.cksum_ragged(d, to_dev(offs, gpu), to_dev(lens, gpu)))
     hb = d[:total].cpu().numpy()
     np.testing.assert_array_equal(got, c_oracle.cksum_ragged(hb, offs, lens, kind=0))
+
+
+@pytest.mark.parametrize("mode", list(RAGGED_MODES))
+@pytest.mark.parametrize("kind,headers", [("ip", False), ("payload", True), ("payload", False)])
+def test_zslots_netmap_ring_mixed_sizes(gpu, monkeypatch, kind, headers, mode):
+    """A netmap RX ring of mixed sizes (backend_netmap.c:379-391): C4's Zipf
+    64-1472 B lengths, one packet per 2048-B slot at +14 (eth.h:44-48) --
+    tools/tune.py --config zslots at 2^18 packets -- with well-formed UDP
+    headers or random bytes read as IP headers; every packet vs the oracle."""
+    ragged_mode(monkeypatch, mode)
+    n = 1 << 18
+    lens = synth.zipf_lengths(n)
+    offs = (np.arange(n, dtype=np.uint64) * 2048 + 14).astype(np.uint64)
+    d = synth_batch(gpu, n * 2048, seed=synth.ZIPF_SEED ^ 14)
+    d_off, d_len = to_dev(offs, gpu), to_dev(lens, gpu)
+    if headers:
+        synth.stamp_udp_headers(d, d_off, d_len)
+    k = 0 if kind == "ip" else 1
+    got = host(wc.cksum_ragged(d, d_off, d_len, kind=kind))
+    hb = d[: n * 2048].cpu().numpy()
+    np.testing.assert_array_equal(got, c_oracle.cksum_ragged(hb, offs, lens, kind=k))
+    if kind == "payload":
+        hdr, pay = wc.cksum_ip_udp_ragged(d, d_off, d_len)
+        np.testing.assert_array_equal(host(pay), c_oracle.cksum_ragged(hb, offs, lens, kind=1))
+        np.testing.assert_array_equal(host(hdr), _ip_hdr_expect_np(hb, offs))
+
+
+def _ip_hdr_expect_np(buf: np.ndarray, offs: np.ndarray) -> np.ndarray:
+    """Vectorised py_oracle.ip_hdr_cksum: ip_cksum(ip, ip4_hl) for IPv4
+    (ip4.c:110-115), 0 for IPv6; hl is a multiple of 4, so whole LE words."""
+    idx = offs.astype(np.int64)[:, None] + np.arange(60, dtype=np.int64)[None, :]
+    b = buf[idx].astype(np.uint32)
+    hl = (b[:, 0] & 15) * 4
+    words = b[:, 0::2] + (b[:, 1::2] << 8)
+    acc = (words * (np.arange(30)[None, :] * 2 < hl[:, None])).sum(axis=1).astype(np.uint64)
+    while (acc > 0xFFFF).any():
+        acc = (acc & 0xFFFF) + (acc >> 16)
+    res = (~acc & 0xFFFF).astype(np.uint16)
+    return np.where(b[:, 0] >> 4 == 4, res, 0).astype(np.uint16)
 
 
 def test_c2_roundtrip_property(gpu):
@@ -499,8 +539,12 @@ def test_c2_roundtrip_property(gpu):
 # ---------------------------------------------------------------------------
 # Host-memory (end-to-end) path and the C drop-in.
 
+@pytest.mark.parametrize("kind", ["ip", "payload"])
 @pytest.mark.parametrize("register", [False, True])
-def test_host_path(gpu, register):
+def test_host_path(gpu, register, kind):
+    """Pipelined host path, > 1 chunk, both kinds (payload_cksum: random
+    bytes read as IPv4/IPv6 headers, every len >= 64 >= hl; max(len, 20)
+    spans and rebased offsets through the seg kernel on the staged bytes)."""
     rng = np.random.default_rng(12)
     lens = synth.zipf_lengths(300000, seed=5)
     offs = synth.packed_offsets(lens, lead=3)
@@ -508,11 +552,12 @@ def test_host_path(gpu, register):
     if register:
         wc.host_register(buf)
     try:
-        got = wc.cksum_host(buf, offs, lens, kind="ip")
+        got = wc.cksum_host(buf, offs, lens, kind=kind)
     finally:
         if register:
             wc.host_unregister(buf)
-    np.testing.assert_array_equal(got, c_oracle.cksum_ragged(buf, offs, lens, kind=0))
+    np.testing.assert_array_equal(
+        got, c_oracle.cksum_ragged(buf, offs, lens, kind=0 if kind == "ip" else 1))
 
 
 @pytest.mark.parametrize("kind", ["ip", "payload"])
@@ -544,17 +589,19 @@ def test_host_zero_copy_small_batches(gpu, kind, n):
     np.testing.assert_array_equal(got, want)
 
 
-def test_host_path_unordered_gather(gpu):
+@pytest.mark.parametrize("kind", ["ip", "payload"])
+def test_host_path_unordered_gather(gpu, kind):
     """Offsets in random order through the pipelined path (gathered into
-    pinned staging), more than one 64 MiB chunk."""
+    pinned staging), more than one 64 MiB chunk, both kinds."""
     rng = np.random.default_rng(13)
     lens = synth.zipf_lengths(400000, seed=6)
     offs = synth.packed_offsets(lens, lead=1)
     buf = rng.integers(0, 256, int(offs[-1]) + int(lens[-1]) + 64, dtype=np.uint8)
     perm = rng.permutation(lens.size)
     offs, lens = offs[perm], lens[perm]
-    got = wc.cksum_host(buf, offs, lens, kind="ip")
-    np.testing.assert_array_equal(got, c_oracle.cksum_ragged(buf, offs, lens, kind=0))
+    got = wc.cksum_host(buf, offs, lens, kind=kind)
+    np.testing.assert_array_equal(
+        got, c_oracle.cksum_ragged(buf, offs, lens, kind=0 if kind == "ip" else 1))
 
 
 def test_host_path_rejects_out_of_range(gpu):

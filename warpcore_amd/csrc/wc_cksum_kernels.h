@@ -83,6 +83,7 @@ struct LaunchArgs {
     // dense tiles | sparse tiles << 8 (65 = never)
     int grp_thr = 65 | (40 << 8);
     int grp_rows = 4; // k_cksum_seg grouped path: rows per ping-pong group (2, 4)
+    int flat_pk = 1;  // flat kernel: 16-byte chunks per lane slot (1, or 2 = 32 B per lane)
 };
 
 struct Shape {

@@ -37,9 +37,9 @@ struct FlatDesc {          // 16 bytes per non-empty packet of the tile, in LDS
     uint32_t info;         // len | hl << 16 | v4 << 24
 };
 
-template <int UN>
+template <int UN, int PK = 1>
 struct FlatRows {
-    u32x4 d[UN];
+    u32x4 d[UN][PK];
     uint32_t own[UN];
 };
 
@@ -57,9 +57,12 @@ __device__ __forceinline__ void wave_order()
     __builtin_amdgcn_wave_barrier();
 }
 
-// Owner lookup + loads for the UN rows of a group starting at slot g0.
-template <int UN, bool NT, bool NOLOAD = false>
-__device__ __forceinline__ void flat_issue(FlatRows<UN> &R, FlatLds<UN> &L,
+// Owner lookup + loads for the UN rows of a group starting at slot g0.  A
+// slot is PK consecutive 16-byte chunks of one packet (PK = 2: every lane
+// streams 32 contiguous bytes per row, and the owner lookup, scan and
+// hand-offs below are paid once per 2 chunks).
+template <int UN, bool NT, bool NOLOAD = false, int PK = 1, int KIND = WC_KIND_IP>
+__device__ __forceinline__ void flat_issue(FlatRows<UN, PK> &R, FlatLds<UN> &L,
                                            uint32_t g0, int lane, uint32_t cp,
                                            uint32_t ce, uint32_t rank,
                                            uint32_t last_rank, uint32_t total)
@@ -89,20 +92,36 @@ __device__ __forceinline__ void flat_issue(FlatRows<UN> &R, FlatLds<UN> &L,
         const bool st = L.mark[u][lane] == (row0 >> 6);
         const uint32_t own = min(first[u] + mbcnt64(__ballot(st)) + (st ? 1u : 0u), last_rank);
         R.own[u] = own;
-        const uint64_t vb = *reinterpret_cast<const uint64_t *>(&L.desc[own]);
         // Unconditional load (slots past the tile's end re-read its last
         // chunk and are zeroed in flat_accum): a straight-line issue stream
         // lets hipcc wait for exactly the older row group.
         const uint32_t q = min(row0 + (uint32_t)lane, total - 1u);
-        if constexpr (NOLOAD) // diagnostic build: same stream, no HBM traffic
-            R.d[u] = u32x4{(uint32_t)vb, q, (uint32_t)(vb >> 32), q ^ 0x5a5a5a5au};
-        else
-            R.d[u] = load_chunk<NT>(vb + 16ull * q);
+        if constexpr (PK == 1) {
+            const uint64_t vb = *reinterpret_cast<const uint64_t *>(&L.desc[own]);
+            if constexpr (NOLOAD) // diagnostic build: same stream, no HBM traffic
+                R.d[u][0] = u32x4{(uint32_t)vb, q, (uint32_t)(vb >> 32), q ^ 0x5a5a5a5au};
+            else
+                R.d[u][0] = load_chunk<NT>(vb + 16ull * q);
+        } else {
+            // The slot's chunks past the packet's last one re-read that
+            // chunk (never a page the packet does not touch); their weights
+            // are zero in flat_accum.
+            const FlatDesc g = L.desc[own];
+            const uint64_t vb = (uint64_t)g.vb_lo | ((uint64_t)g.vb_hi << 32);
+            const uint32_t len = g.info & 0xFFFFu;
+            const uint32_t span = KIND == WC_KIND_PAYLOAD ? max(len, 20u) : len;
+            const uint32_t cend = (g.rel >> 4) + (((g.rel & 15u) + span + 15u) >> 4);
+#pragma unroll
+            for (int j = 0; j < PK; ++j) {
+                const uint32_t c = min((uint32_t)PK * q + (uint32_t)j, cend - 1u);
+                R.d[u][j] = load_chunk<NT>(vb + 16ull * c);
+            }
+        }
     }
 }
 
-template <int UN, int KIND, bool ARITH = false>
-__device__ __forceinline__ void flat_accum(const FlatRows<UN> &R, FlatLds<UN> &L,
+template <int UN, int KIND, bool ARITH = false, int PK = 1>
+__device__ __forceinline__ void flat_accum(const FlatRows<UN, PK> &R, FlatLds<UN> &L,
                                            const WeightLut *M, uint32_t g0,
                                            int lane, uint32_t cp, uint32_t ce,
                                            uint32_t total, uint32_t &acc)
@@ -114,12 +133,16 @@ __device__ __forceinline__ void flat_accum(const FlatRows<UN> &R, FlatLds<UN> &L
         const FlatDesc &g = L.desc[R.own[u]];
         const uint32_t rel = g.rel, info = g.info;
         uint32_t E = 0, O = 0;
-        if constexpr (ARITH)
-            accum_arith<KIND>(R.d[u], (int)(16u * q - rel), (int)((info >> 16) & 0xFFu),
-                              (int)(info & 0xFFFFu), (info >> 24) & 1u, E, O);
-        else
-            accum_masked<KIND>(R.d[u], (int)(16u * q - rel), (int)((info >> 16) & 0xFFu),
-                               (int)(info & 0xFFFFu), (info >> 24) & 1u, *M, E, O);
+#pragma unroll
+        for (int j = 0; j < PK; ++j) {
+            const int co = (int)(16u * ((uint32_t)PK * q + (uint32_t)j) - rel);
+            if constexpr (ARITH)
+                accum_arith<KIND>(R.d[u][j], co, (int)((info >> 16) & 0xFFu),
+                                  (int)(info & 0xFFFFu), (info >> 24) & 1u, E, O);
+            else
+                accum_masked<KIND>(R.d[u][j], co, (int)((info >> 16) & 0xFFu),
+                                   (int)(info & 0xFFFFu), (info >> 24) & 1u, *M, E, O);
+        }
         P[u] = q < total ? combine(E, O, rel & 1u) : 0u;
     }
     // Inclusive prefix sums of the UN rows, step-interleaved so each row's DPP
@@ -221,27 +244,30 @@ __device__ __forceinline__ uint16_t lane_hdr_cksum(uint64_t a, uint32_t hl,
 // reference accumulator (in_cksum.c:140-167 / 107-120, mod 2^32) -- the
 // caller folds it.  `after_first_issue` runs once the tile's first row group
 // is in flight (the caller's next-tile prefetch goes there).
-template <int UN, int KIND, bool NT, bool NOLOAD, bool ARITH, class F>
+template <int UN, int KIND, bool NT, bool NOLOAD, bool ARITH, class F, int PK = 1>
 __device__ __forceinline__ uint32_t flat_tile_sum(FlatLds<UN> &L, const WeightLut *lut,
                                                   int lane, uint64_t a, uint32_t len,
                                                   bool valid, const PseudoHdr &ph,
                                                   F &&after_first_issue)
 {
+    static_assert(PK == 1 || !NOLOAD, "diagnostic build: one chunk per slot");
     const uint32_t s = (uint32_t)(a & 15u);
     const uint32_t span = KIND == WC_KIND_PAYLOAD ? max(len, 20u) : len;
     const uint32_t nch = valid ? (s + span + 15u) >> 4 : 0u;
+    const uint32_t nsl = (nch + PK - 1u) / PK; // slots of PK chunks
 
-    // Chunk-slot range [cp, ce) of this lane's packet within the tile;
-    // rank among the tile's non-empty packets.
-    const uint32_t ce = wave_incl_sum(nch);
-    const uint32_t cp = ce - nch;
+    // Slot range [cp, ce) of this lane's packet within the tile; rank among
+    // the tile's non-empty packets.  Slot q's chunk j is the packet's chunk
+    // PK (q - cp) + j, at vb + 16 (PK q + j).
+    const uint32_t ce = wave_incl_sum(nsl);
+    const uint32_t cp = ce - nsl;
     const uint32_t total = lane_u32(ce, 63);
     const uint64_t nonempty = __ballot(nch != 0);
     const uint32_t rank = mbcnt64(nonempty);
     const uint32_t last_rank = nonempty ? (uint32_t)__builtin_popcountll(nonempty) - 1u : 0u;
-    const uint64_t vb = (a & ~15ull) - 16ull * cp;
+    const uint64_t vb = (a & ~15ull) - 16ull * PK * cp;
     if (nch != 0)
-        L.desc[rank] = FlatDesc{(uint32_t)vb, (uint32_t)(vb >> 32), s + 16u * cp,
+        L.desc[rank] = FlatDesc{(uint32_t)vb, (uint32_t)(vb >> 32), s + 16u * PK * cp,
                                 len | (ph.hl << 16) | (ph.v4 << 24)};
     // Row marks carry the row's number within the tile; reset them to a
     // tag no row has so the previous tile's marks can't match.
@@ -252,9 +278,9 @@ __device__ __forceinline__ uint32_t flat_tile_sum(FlatLds<UN> &L, const WeightLu
 
     uint32_t acc = ph.special;
     constexpr uint32_t kGrp = 64u * UN;
-    FlatRows<UN> A, B;
+    FlatRows<UN, PK> A, B;
     if (total != 0)
-        flat_issue<UN, NT, NOLOAD>(A, L, 0, lane, cp, ce, rank, last_rank, total);
+        flat_issue<UN, NT, NOLOAD, PK, KIND>(A, L, 0, lane, cp, ce, rank, last_rank, total);
     after_first_issue();
     if (total != 0) {
         // Ping-pong row groups A / B (no register copies): group g+1's
@@ -264,13 +290,15 @@ __device__ __forceinline__ uint32_t flat_tile_sum(FlatLds<UN> &L, const WeightLu
         // next to it; sched_barrier keeps each issue ahead of the other
         // group's sum.
         for (uint32_t j = 0; j < total; j += 2 * kGrp) {
-            flat_issue<UN, NT, NOLOAD>(B, L, j + kGrp, lane, cp, ce, rank, last_rank, total);
+            flat_issue<UN, NT, NOLOAD, PK, KIND>(B, L, j + kGrp, lane, cp, ce, rank, last_rank,
+                                                 total);
             __builtin_amdgcn_sched_barrier(0);
-            flat_accum<UN, KIND, ARITH>(A, L, lut, j, lane, cp, ce, total, acc);
+            flat_accum<UN, KIND, ARITH, PK>(A, L, lut, j, lane, cp, ce, total, acc);
             __builtin_amdgcn_sched_barrier(0);
-            flat_issue<UN, NT, NOLOAD>(A, L, j + 2 * kGrp, lane, cp, ce, rank, last_rank, total);
+            flat_issue<UN, NT, NOLOAD, PK, KIND>(A, L, j + 2 * kGrp, lane, cp, ce, rank,
+                                                 last_rank, total);
             __builtin_amdgcn_sched_barrier(0);
-            flat_accum<UN, KIND, ARITH>(B, L, lut, j + kGrp, lane, cp, ce, total, acc);
+            flat_accum<UN, KIND, ARITH, PK>(B, L, lut, j + kGrp, lane, cp, ce, total, acc);
             __builtin_amdgcn_sched_barrier(0);
         }
     }

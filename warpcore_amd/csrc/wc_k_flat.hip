@@ -5,7 +5,7 @@
 
 namespace wc {
 
-template <int UN, int KIND, bool NT, bool HDR, bool NOLOAD = false>
+template <int UN, int KIND, bool NT, bool HDR, bool NOLOAD = false, int PK = 1>
 __global__ void __launch_bounds__(256)
 k_cksum_flat(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
              const uint16_t *__restrict__ lens, uint64_t n,
@@ -54,11 +54,12 @@ k_cksum_flat(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
                 ph = hdr_pseudo(hdr, a);
         // The next tile's header bytes: issued once its offsets are back,
         // behind this tile's first loads.
-        const uint32_t acc = flat_tile_sum<UN, KIND, NT, NOLOAD, false>(
-            L, &lut, lane, a, len, valid, ph, [&] {
-                if constexpr (KIND == WC_KIND_PAYLOAD)
-                    hdr_n = load_hdr((uint64_t)base + off_n);
-            });
+        auto next_hdr = [&] {
+            if constexpr (KIND == WC_KIND_PAYLOAD)
+                hdr_n = load_hdr((uint64_t)base + off_n);
+        };
+        const uint32_t acc = flat_tile_sum<UN, KIND, NT, NOLOAD, false, decltype(next_hdr) &, PK>(
+            L, &lut, lane, a, len, valid, ph, next_hdr);
 
         const uint16_t r = fold_not(acc);
         if (valid && out)
@@ -87,8 +88,12 @@ static hipError_t launch_flat_un(const LaunchArgs &a, hipStream_t st)
     const uint8_t *b = (const uint8_t *)a.base;
     unsigned long long *bad = (unsigned long long *)a.bad;
 #define WC_FLAT(K, N, H)                                                       \
-    hipLaunchKernelGGL((k_cksum_flat<UN, K, N, H>), dim3(grid), dim3(256), 0,  \
-                       st, b, a.offs, a.lens, a.n, a.out, bad, a.out_hdr)
+    if (a.flat_pk == 2)                                                        \
+        hipLaunchKernelGGL((k_cksum_flat<UN, K, N, H, false, 2>), dim3(grid), dim3(256), 0, \
+                           st, b, a.offs, a.lens, a.n, a.out, bad, a.out_hdr); \
+    else                                                                       \
+        hipLaunchKernelGGL((k_cksum_flat<UN, K, N, H>), dim3(grid), dim3(256), 0, st, b, \
+                           a.offs, a.lens, a.n, a.out, bad, a.out_hdr)
     if (a.diag_noload && a.kind == WC_KIND_IP) {
         hipLaunchKernelGGL((k_cksum_flat<UN, WC_KIND_IP, true, false, true>), dim3(grid),
                            dim3(256), 0, st, b, a.offs, a.lens, a.n, a.out, bad, a.out_hdr);
