@@ -49,7 +49,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4", "c5", "slots"])
+    ap.add_argument("--config", default="c2",
+                    choices=["c2", "c3", "c4", "c5", "slots", "zslots"])
     ap.add_argument("--len", type=int, default=1472, help="packet bytes for c3")
     ap.add_argument("--kind", default="ip", choices=["ip", "payload"],
                     help="ip_cksum (default) or payload_cksum per packet")
@@ -181,11 +182,20 @@ def make_workload(args, dev, rank, world):
                 if args.config == "c2" else f"C3: {n} x {L} B packets, stride {L}")
         meta = {"packets_per_gpu": n, "packet_bytes": L, "layout": "strided", "kind": kind}
         return step, n, nbytes, buf, out, plan, desc, meta, (L, L), "weak"
-    if args.config == "slots":
-        n, L, slot, at = args.packets, args.len + 28, 2048, 14
+    if args.config in ("slots", "zslots"):
+        # netmap RX ring drained into one ragged batch: one IP packet per
+        # 2048-B slot at +14 (eth.h:44-48); slots = fixed --len + 28 B,
+        # zslots = C4's Zipf 64-1472 B lengths (a ring of mixed sizes)
+        slot, at = 2048, 14
+        if args.config == "slots":
+            n = args.packets
+            lens = np.full(n, args.len + 28, dtype=np.uint16)
+        else:
+            n = 1 << 21 if args.packets == (1 << 20) else args.packets
+            lens = synth.zipf_lengths(n, seed=synth.ZIPF_SEED + rank)
+        L = int(lens[0])
         offs = (np.arange(n, dtype=np.uint64) * slot + at).astype(np.uint64)
-        lens = np.full(n, L, dtype=np.uint16)
-        nbytes = n * L
+        nbytes = int(lens.astype(np.uint64).sum())
         buf = torch.empty(n * slot + 64, dtype=torch.uint8, device=dev)
         wc.synth_fill(buf, seed, nbytes=n * slot)
         d_off = torch.from_numpy(offs).to(dev)
@@ -199,10 +209,16 @@ def make_workload(args, dev, rank, world):
         def step():
             wc.cksum_ragged(buf, d_off, d_len, out=out, kind=kind, check=False)
 
-        desc = (f"netmap RX ring: {n} x {L} B IP packets in {slot}-B slots at +{at}, "
-                f"ragged batch")
-        meta = {"packets_per_gpu": n, "packet_bytes": L, "slot_bytes": slot,
-                "layout": "ragged", "kind": kind}
+        if args.config == "slots":
+            desc = (f"netmap RX ring: {n} x {L} B IP packets in {slot}-B slots at +{at}, "
+                    f"ragged batch")
+            meta = {"packets_per_gpu": n, "packet_bytes": L, "slot_bytes": slot,
+                    "layout": "ragged", "kind": kind}
+        else:
+            desc = (f"netmap RX ring of mixed sizes: {n} Zipf(s=1) 64-1472 B packets "
+                    f"(mean {nbytes / n:.1f}) in {slot}-B slots at +{at}, ragged batch")
+            meta = {"packets_per_gpu": n, "mean_packet_bytes": round(nbytes / n, 2),
+                    "slot_bytes": slot, "layout": "ragged", "kind": kind}
         plan = {"kernel": "seg (grouped path for uniform tiles)",
                 "rows_per_group": int(os.environ.get("WC_GRP_ROWS", "4")),
                 "grid": int((n + 255) // 256)}

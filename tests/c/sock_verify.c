@@ -17,8 +17,13 @@
  * Test infrastructure: it links the CPU oracle (oracle/wc_oracle.c) to check
  * the GPU results bit-exact on every payload as well.
  *
- * usage: sock_verify [-s len] [-b batch] [-l loops]
- * prints one JSON line.
+ * usage: sock_verify [-s len] [-b batch] [-l loops] [-t prefix]
+ * prints one JSON line.  With -t, every timed iteration is also written in
+ * sockping's TSV format (bin/ping.c:215, 301-302: iface driver mbps byte pkts
+ * tx rx, nanoseconds; "lo" / "lo" / UINT32_MAX for the loopback interface,
+ * as plat_get_iface_driver / plat_get_mbps report it) to prefix.off.tsv
+ * (verify off) and prefix.on.tsv (verify on), so the rows plot with
+ * misc/plot.r next to the reference's own.
  */
 #define _GNU_SOURCE
 #include <arpa/inet.h>
@@ -131,13 +136,29 @@ static double median(uint64_t *v, int n)
 int main(int argc, char **argv)
 {
     int len = 1472, batch = 1, loops = 2000, opt;
-    while ((opt = getopt(argc, argv, "s:b:l:")) != -1) {
+    const char *tsv = NULL;
+    while ((opt = getopt(argc, argv, "s:b:l:t:")) != -1) {
         if (opt == 's')
             len = atoi(optarg);
         else if (opt == 'b')
             batch = atoi(optarg);
         else if (opt == 'l')
             loops = atoi(optarg);
+        else if (opt == 't')
+            tsv = optarg;
+    }
+    FILE *tsv_f[2] = {NULL, NULL};
+    if (tsv) {
+        char path[4096];
+        for (int v = 0; v < 2; v++) {
+            snprintf(path, sizeof path, "%s.%s.tsv", tsv, v ? "on" : "off");
+            tsv_f[v] = fopen(path, "w");
+            if (!tsv_f[v]) {
+                fprintf(stderr, "sock_verify: cannot write %s\n", path);
+                return 2;
+            }
+            fputs("iface\tdriver\tmbps\tbyte\tpkts\ttx\trx\n", tsv_f[v]); /* ping.c:215 */
+        }
     }
     if (len < 0 || len > SLOT - 16 || batch < 1 || batch > RECV_SIZE || loops < 2) {
         fprintf(stderr, "sock_verify: bad arguments\n");
@@ -202,6 +223,7 @@ int main(int argc, char **argv)
                 break;
             sent += k;
         }
+        const uint64_t t_tx = now_ns();
 
         /* RX: w_rx-style recvmmsg into free slots of the upper half (in
          * reverse pool order, as a free list returns them), until the batch
@@ -237,6 +259,15 @@ int main(int argc, char **argv)
             t_v = now_ns() - v0;
         }
         const uint64_t t1 = now_ns();
+        if (tsv_f[verify]) /* ping.c:301-302: rx is "NA" for a lost round trip */
+            fprintf(tsv_f[verify], "lo\tlo\t%u\t%u\t%d\t%llu\t", 0xFFFFFFFFu,
+                    got ? (unsigned)rx_len[0] : 0u, got, (unsigned long long)(t_tx - t0));
+        if (tsv_f[verify]) {
+            if (got == batch)
+                fprintf(tsv_f[verify], "%llu\n", (unsigned long long)(t1 - t0));
+            else
+                fputs("NA\n", tsv_f[verify]);
+        }
         if (got < batch)
             continue;
         if (verify) {
@@ -260,6 +291,9 @@ int main(int argc, char **argv)
     close(cli);
     close(srv);
     wc_host_unregister(pool);
+    for (int v = 0; v < 2; v++)
+        if (tsv_f[v])
+            fclose(tsv_f[v]);
 
     printf("{\"config\": \"sockping->echo loopback\", \"len\": %d, \"batch\": %d, "
            "\"loops\": %d, \"rtt_ns_median_verify_off\": %.0f, "

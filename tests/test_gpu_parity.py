@@ -699,12 +699,22 @@ def test_socket_rx_verify_pass(gpu, tmp_path, batch, length):
     4): echo over loopback, every received payload checksummed by the GPU in
     place from the registered pool and matched against TX and the oracle."""
     exe = build_sock_verify(tmp_path / "sock_verify")
-    r = subprocess.run([str(exe), "-s", str(length), "-b", str(batch), "-l", "200"],
+    r = subprocess.run([str(exe), "-s", str(length), "-b", str(batch), "-l", "200",
+                        "-t", str(tmp_path / "ping")],
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert res["gpu_mismatch"] == 0 and res["oracle_mismatch"] == 0
     assert res["packets_verified"] >= 50 * batch
+    # sockping's TSV (bin/ping.c:215, 301-302), one row per round trip
+    for v in ("off", "on"):
+        rows = (tmp_path / f"ping.{v}.tsv").read_text().splitlines()
+        assert rows[0] == "iface\tdriver\tmbps\tbyte\tpkts\ttx\trx"
+        assert len(rows) == 1 + 100
+        for row in rows[1:]:
+            f = row.split("\t")
+            assert f[:3] == ["lo", "lo", "4294967295"] and len(f) == 7
+            assert f[6] == "NA" or (int(f[3]) == length and int(f[4]) == batch and int(f[6]) > 0)
 
 
 # ---------------------------------------------------------------------------

@@ -6,7 +6,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export WC_NO_BUILD=1 TMPDIR=/tmp
-TAG=${TAG:-r01}
+TAG=${TAG:-r02}
 mkdir -p gpurun_out/round
 for c in ${CFGS:-c2 c4 c4pl slotspl}; do
     case $c in
@@ -18,6 +18,9 @@ for c in ${CFGS:-c2 c4 c4pl slotspl}; do
         slots) a="--config slots" ;;
         slotspl) a="--config slots --kind payload --headers" ;;
         c5) a="--config c5" ;;
+        c3_*) a="--config c3 --len ${c#c3_}" ;;
+        zslots) a="--config zslots" ;;
+        zslotspl) a="--config zslots --kind payload --headers" ;;
         *) echo "unknown config $c"; exit 2 ;;
     esac
     echo "== $c: bench"
