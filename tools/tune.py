@@ -18,6 +18,7 @@ import os
 import statistics
 import subprocess
 import sys
+import time
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
@@ -64,6 +65,9 @@ def main():
     ap.add_argument("--ceiling", action="store_true")
     ap.add_argument("--json", default="")
     ap.add_argument("--verbose", action="store_true", help="print every round's time")
+    ap.add_argument("--warm-ms", type=float, default=30.0,
+                    help="run each variant this long (untimed) before its timed launches, "
+                         "so a small batch is timed at ramped clocks")
     ap.add_argument("--kind", default="ip", choices=["ip", "payload"])
     ap.add_argument("--offset", type=int, default=0, help="byte offset of packet 0 (c2/c3)")
     ap.add_argument("--stride", type=int, default=0, help="packet stride (c2/c3; default len)")
@@ -166,6 +170,11 @@ def main():
                     print(f"!! variant {name!r} skipped: {e}", flush=True)
                     times[name].append(float("inf"))
                     continue
+                t_w = time.perf_counter()
+                while (time.perf_counter() - t_w) * 1e3 < args.warm_ms:
+                    for _ in range(8):
+                        run()
+                    torch.cuda.synchronize()
                 ms = time_it(run, args.iters, stream)
                 if r == 0:
                     res = out.cpu().numpy().view(np.uint16).copy()

@@ -219,6 +219,34 @@ __device__ __forceinline__ PseudoHdr hdr_pseudo(const HdrRaw &h, uint64_t a)
     return pseudo_hdr(h0 & 0xFFu, (h0 >> 8) & 0xFFu, (h0 >> 16) & 0xFFu, h0 >> 24);
 }
 
+// payload_cksum as an ip_cksum-style sum over [8, len) plus per-packet terms.
+// The pseudo-header's src/dst fields end where a standard header ends (IPv4
+// @12..19 with IHL 5, IPv6 @8..39, in_cksum.c:150-151, 158-159), so the
+// reference's accumulator (in_cksum.c:140-164) is, exactly and mod 2^32:
+//   IPv4, hl = 20:  words[8, len) - (b8 + b10 + (b11 << 8)) + special
+//                   (words[8, 12) = b8 + (b9 << 8) + b10 + (b11 << 8), and the
+//                   reference adds proto = b9 << 8 itself, in_cksum.c:149)
+//   IPv6:           words[8, len) + (b4 | b5 << 8) + special   (in_cksum.c:160)
+// where words[...] are little-endian 16-bit words counted from the packet
+// start (8 is even, so the flat path's exact byte-lane sums E / O combine to
+// them) and special is the plen re-swap / next_hdr << 24 term.  Chunks then
+// need only the range masks of ip_cksum -- no pseudo-header weight tables --
+// which is half the masking work of the generic payload accumulate.  Returns
+// false (generic path) for an IPv4 header with options or a malformed IHL,
+// and for a packet shorter than its header.
+__device__ __forceinline__ bool payload_as_ip(const HdrRaw &h, uint64_t a, uint32_t len,
+                                              const PseudoHdr &ph, uint32_t &extra)
+{
+    const uint32_t sh = 8u * (uint32_t)(a & 3u);
+    const uint32_t w1 = __builtin_amdgcn_alignbit(h.d.z, h.d.y, sh); // bytes 4..7
+    const uint32_t w2 = __builtin_amdgcn_alignbit(h.d.w, h.d.z, sh); // bytes 8..11
+    if (ph.v4)
+        extra = ph.special - ((w2 & 0xFFu) + ((w2 >> 16) & 0xFFu) + ((w2 >> 24) << 8));
+    else
+        extra = ph.special + (w1 & 0xFFFFu);
+    return ph.v4 ? (ph.hl == 20u && len >= 20u) : len >= 40u;
+}
+
 // Fused IPv4 header checksum for the flat kernel: the packet's own lane sums
 // its header [0, hl) (at most 5 chunks) -- ip_cksum(ip, hl), ip4.c:110-115.
 template <bool NT>
@@ -284,11 +312,12 @@ __device__ __forceinline__ uint32_t flat_tile_sum(FlatLds<UN> &L, const WeightLu
     after_first_issue();
     if (total != 0) {
         // Ping-pong row groups A / B (no register copies): group g+1's
-        // loads are in flight while group g is summed.  No exit between
-        // the halves: a half past the tile's end sums zeros, and keeping
-        // each load's use in the next half stops hipcc sinking the load
-        // next to it; sched_barrier keeps each issue ahead of the other
-        // group's sum.
+        // loads are in flight while group g is summed; sched_barrier keeps
+        // each issue ahead of the other group's sum.
+        // No exit between the halves: a half past the tile's end sums
+        // zeros, and a single loop exit keeps hipcc's waits precise (a
+        // mid-loop exit left the second group's loads pending at the loop
+        // head, where hipcc then waited vmcnt(0) on every iteration).
         for (uint32_t j = 0; j < total; j += 2 * kGrp) {
             flat_issue<UN, NT, NOLOAD, PK, KIND>(B, L, j + kGrp, lane, cp, ce, rank, last_rank,
                                                  total);
@@ -303,6 +332,25 @@ __device__ __forceinline__ uint32_t flat_tile_sum(FlatLds<UN> &L, const WeightLu
         }
     }
     return acc;
+}
+
+// flat_tile_sum for payload_cksum batches: a tile whose packets all pass
+// payload_as_ip runs as ip_cksum over [8, len) with per-packet terms (the
+// range start 8 rides in the descriptor's hl field); any other tile takes
+// the generic payload accumulate.  Tile-uniform choice.
+template <int UN, bool NT, bool ARITH, class F, int PK = 1>
+__device__ __forceinline__ uint32_t flat_tile_sum_payload(FlatLds<UN> &L, const WeightLut *lut,
+                                                          int lane, uint64_t a, uint32_t len,
+                                                          bool valid, const PseudoHdr &ph,
+                                                          const HdrRaw &hdr, F &&after_first_issue)
+{
+    uint32_t extra = 0;
+    const bool fast = !valid || payload_as_ip(hdr, a, len, ph, extra);
+    if (!__ballot(!fast))
+        return flat_tile_sum<UN, WC_KIND_IP, NT, false, ARITH, F, PK>(
+            L, lut, lane, a, len, valid, PseudoHdr{8u, 0u, extra}, (F &&)after_first_issue);
+    return flat_tile_sum<UN, WC_KIND_PAYLOAD, NT, false, ARITH, F, PK>(
+        L, lut, lane, a, len, valid, ph, (F &&)after_first_issue);
 }
 
 } // namespace

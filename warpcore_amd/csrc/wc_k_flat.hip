@@ -58,8 +58,13 @@ k_cksum_flat(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
             if constexpr (KIND == WC_KIND_PAYLOAD)
                 hdr_n = load_hdr((uint64_t)base + off_n);
         };
-        const uint32_t acc = flat_tile_sum<UN, KIND, NT, NOLOAD, false, decltype(next_hdr) &, PK>(
-            L, &lut, lane, a, len, valid, ph, next_hdr);
+        uint32_t acc;
+        if constexpr (KIND == WC_KIND_PAYLOAD && !NOLOAD)
+            acc = flat_tile_sum_payload<UN, NT, false, decltype(next_hdr) &, PK>(
+                L, &lut, lane, a, len, valid, ph, hdr, next_hdr);
+        else
+            acc = flat_tile_sum<UN, KIND, NT, NOLOAD, false, decltype(next_hdr) &, PK>(
+                L, &lut, lane, a, len, valid, ph, next_hdr);
 
         const uint16_t r = fold_not(acc);
         if (valid && out)

@@ -619,12 +619,19 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
                                              zero, done, rh);
         if (!done) {
             PseudoHdr ph{0u, 1u, 0u};
-            if constexpr (KIND == WC_KIND_PAYLOAD)
+            HdrRaw hdr{};
+            if constexpr (KIND == WC_KIND_PAYLOAD) {
+                hdr = load_hdr(a);
                 if (valid)
-                    ph = hdr_pseudo(load_hdr(a), a);
+                    ph = hdr_pseudo(hdr, a);
+            }
             wave_order();
-            r = fold_not(flat_tile_sum<UN, KIND, NT, false, true>(L.flat, nullptr, lane, a, len,
-                                                                  valid, ph, [] {}));
+            if constexpr (KIND == WC_KIND_PAYLOAD)
+                r = fold_not(flat_tile_sum_payload<UN, NT, true>(L.flat, nullptr, lane, a, len,
+                                                                 valid, ph, hdr, [] {}));
+            else
+                r = fold_not(flat_tile_sum<UN, KIND, NT, false, true>(L.flat, nullptr, lane, a,
+                                                                      len, valid, ph, [] {}));
             if constexpr (HDR)
                 rh = valid && ph.v4 ? lane_hdr_cksum<NT>(a, ph.hl, nullptr) : (uint16_t)0;
         }
