@@ -94,13 +94,12 @@ struct Config {
     wc::Shape shape{};
     bool have_rshape = false;      // WC_RAGGED_SHAPE: small ragged group shape
     wc::Shape rshape{};
-    int strided_seg = 1;           // WC_STRIDED_SEG: 0 never, 1 by size, 2 always
-    int sseg_minch = 7;            // WC_STRIDED_SEG_MINCH
-    int sseg_maxch = 48;           // WC_STRIDED_SEG_MAXCH
+    int strided_seg = 1;           // WC_STRIDED_SEG: 0 never, 1 by the table, 2 always
     int flat_un = 2;               // WC_FLAT_UN: flat kernel rows per group
     int flat_tpw = 1;              // WC_FLAT_TPW: flat kernel tiles per wave
     int seg = 1;                   // WC_SEG: 0 = flat kernel for ragged batches
-    int seg_rows = 4;              // WC_SEG_ROWS
+    int seg_rows = 4;              // WC_SEG_ROWS (ragged; packed strided: set = forced)
+    bool seg_rows_set = false;
     int zc_seg = 0;                // WC_ZC_SEG: seg kernel on zero-copy batches
     int zc_group_max = (int)kZcGroupMax; // WC_ZC_GROUP_MAX
     int zc_bytes = kZcBytesDefault;      // WC_ZC_BYTES
@@ -160,12 +159,11 @@ void load_config_locked()
     c.have_shape = parse_shape(getenv("WC_SHAPE"), &c.shape);
     c.have_rshape = parse_shape(getenv("WC_RAGGED_SHAPE"), &c.rshape);
     c.strided_seg = env_int("WC_STRIDED_SEG", c.strided_seg);
-    c.sseg_minch = env_int("WC_STRIDED_SEG_MINCH", c.sseg_minch);
-    c.sseg_maxch = env_int("WC_STRIDED_SEG_MAXCH", c.sseg_maxch);
     c.flat_un = env_int("WC_FLAT_UN", c.flat_un);
     c.flat_tpw = env_int("WC_FLAT_TPW", c.flat_tpw);
     c.seg = env_int("WC_SEG", c.seg);
     c.seg_rows = env_int("WC_SEG_ROWS", c.seg_rows);
+    c.seg_rows_set = getenv("WC_SEG_ROWS") && *getenv("WC_SEG_ROWS");
     c.zc_seg = env_int("WC_ZC_SEG", c.zc_seg);
     c.zc_group_max = env_int("WC_ZC_GROUP_MAX", c.zc_group_max);
     c.zc_bytes = env_int("WC_ZC_BYTES", c.zc_bytes);
@@ -331,17 +329,23 @@ Plan plan_strided(const Device &D, const Config &C, uint64_t base, uint64_t stri
     p.grid = grid_for(D, C, p.shape, n);
     // Packed (or nearly packed) packets that the group kernel would have to
     // mask: the seg kernel streams their byte range instead (k_cksum_seg<STR>)
-    // -- measured better from 7 to 48 chunks per packet (256 B at +14: 59 ->
-    // 78 % of HBM peak, 576 B at +14: 77 -> 83 %), worse at MTU size (88 ->
-    // 85 %) and for tiny packets.  WC_STRIDED_SEG = 0
-    // never, 2 always (no fused header), 1 = chunk counts in
-    // [WC_STRIDED_SEG_MINCH, WC_STRIDED_SEG_MAXCH].
+    // where it measured faster -- a 60-length x 2-offset sweep on MI355X
+    // (profiles/sweep_r02_planner.log):
+    //   stride % 64 == 0   group kernel (every packet at the same offset in
+    //                      its cache lines: 256 B at +14 85 % vs seg 70-73 %)
+    //   <= 5 chunks        group kernel
+    //   6..14 chunks       seg, 2-row groups (120 B: 74 % vs group 51-56 %)
+    //   36..48 chunks      group kernel (550-700 B: 84-89 % vs seg 83-84 %)
+    //   >= 90 chunks       group kernel
+    //   otherwise          seg, 4-row groups (300 B: 84 % vs group 69 %)
+    // WC_STRIDED_SEG = 0 never, 2 always (no fused header), 1 = the table;
+    // WC_SEG_ROWS forces the row-group size.
     const int sseg = C.strided_seg;
     const bool packed = len != 0 && stride >= len && stride <= len + len / 8u;
-    const bool seg_size = nch >= (uint32_t)C.sseg_minch && nch <= (uint32_t)C.sseg_maxch;
-    if (!hdr && !p.full && n >= 64 && packed && (sseg == 2 || (sseg == 1 && seg_size))) {
+    const bool seg_table = stride % 64 != 0 && nch > 5 && !(nch >= 36 && nch <= 48) && nch < 90;
+    if (!hdr && !p.full && n >= 64 && packed && (sseg == 2 || (sseg == 1 && seg_table))) {
         p.shape = {0, 1, C.flat_un};
-        p.seg_rows = C.seg_rows;
+        p.seg_rows = C.seg_rows_set ? C.seg_rows : (nch <= 14 ? 2 : 4);
         p.grid = 0;
     }
     return p;

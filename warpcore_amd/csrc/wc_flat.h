@@ -314,11 +314,12 @@ __device__ __forceinline__ uint32_t flat_tile_sum(FlatLds<UN> &L, const WeightLu
         // Ping-pong row groups A / B (no register copies): group g+1's
         // loads are in flight while group g is summed; sched_barrier keeps
         // each issue ahead of the other group's sum.
-        // No exit between the halves: a half past the tile's end sums
-        // zeros, and a single loop exit keeps hipcc's waits precise (a
-        // mid-loop exit left the second group's loads pending at the loop
-        // head, where hipcc then waited vmcnt(0) on every iteration).
-        for (uint32_t j = 0; j < total; j += 2 * kGrp) {
+        // While a third group still holds tile slots; then a tail of one
+        // or two groups.  Every issued group is summed: a load left pending
+        // at the loop's exit makes hipcc wait vmcnt(0) at the loop head on
+        // every iteration (measured in the ISA with a mid-loop exit).
+        uint32_t j = 0;
+        for (; j + 2 * kGrp < total; j += 2 * kGrp) {
             flat_issue<UN, NT, NOLOAD, PK, KIND>(B, L, j + kGrp, lane, cp, ce, rank, last_rank,
                                                  total);
             __builtin_amdgcn_sched_barrier(0);
@@ -329,6 +330,16 @@ __device__ __forceinline__ uint32_t flat_tile_sum(FlatLds<UN> &L, const WeightLu
             __builtin_amdgcn_sched_barrier(0);
             flat_accum<UN, KIND, ARITH, PK>(B, L, lut, j + kGrp, lane, cp, ce, total, acc);
             __builtin_amdgcn_sched_barrier(0);
+        }
+        if (j + kGrp < total) {
+            flat_issue<UN, NT, NOLOAD, PK, KIND>(B, L, j + kGrp, lane, cp, ce, rank, last_rank,
+                                                 total);
+            __builtin_amdgcn_sched_barrier(0);
+            flat_accum<UN, KIND, ARITH, PK>(A, L, lut, j, lane, cp, ce, total, acc);
+            __builtin_amdgcn_sched_barrier(0);
+            flat_accum<UN, KIND, ARITH, PK>(B, L, lut, j + kGrp, lane, cp, ce, total, acc);
+        } else {
+            flat_accum<UN, KIND, ARITH, PK>(A, L, lut, j, lane, cp, ce, total, acc);
         }
     }
     return acc;

@@ -231,8 +231,13 @@ __device__ __forceinline__ uint16_t seg_tile(uint32_t *pre, u32x4 *stage, int la
     uint32_t carry = 0, Ps = 0, Pe = 0;
     u32x4 hs = {0u, 0u, 0u, 0u}, he = {0u, 0u, 0u, 0u}, h1 = {0u, 0u, 0u, 0u},
           h2 = {0u, 0u, 0u, 0u};
+    // Ping-pong row groups A / B while a third group still holds tile
+    // chunks; then a tail of one or two groups.  Every issued group is
+    // summed (no load is left pending, so hipcc's waits stay precise) and
+    // the rows summed round up to one group, not two (a 17-row tile sums
+    // 20 rows instead of 24).
     uint32_t j = 0;
-    for (; j < T; j += 2 * kGrp) {
+    for (; j + 2 * kGrp < T; j += 2 * kGrp) {
         seg_issue<UNS, NT>(B, A0, j + kGrp, lane, T, zero);
         __builtin_amdgcn_sched_barrier(0);
         seg_accum<UNS, HC>(A, pre, stage, j, lane, cs, ce, c0, carry, Ps, Pe, hs, he, h1, h2);
@@ -242,6 +247,18 @@ __device__ __forceinline__ uint16_t seg_tile(uint32_t *pre, u32x4 *stage, int la
         seg_accum<UNS, HC>(B, pre, stage, j + kGrp, lane, cs, ce, c0, carry, Ps, Pe, hs, he, h1,
                            h2);
         __builtin_amdgcn_sched_barrier(0);
+    }
+    if (j + kGrp < T) {
+        seg_issue<UNS, NT>(B, A0, j + kGrp, lane, T, zero);
+        __builtin_amdgcn_sched_barrier(0);
+        seg_accum<UNS, HC>(A, pre, stage, j, lane, cs, ce, c0, carry, Ps, Pe, hs, he, h1, h2);
+        __builtin_amdgcn_sched_barrier(0);
+        seg_accum<UNS, HC>(B, pre, stage, j + kGrp, lane, cs, ce, c0, carry, Ps, Pe, hs, he, h1,
+                           h2);
+        j += 2 * kGrp;
+    } else {
+        seg_accum<UNS, HC>(A, pre, stage, j, lane, cs, ce, c0, carry, Ps, Pe, hs, he, h1, h2);
+        j += kGrp;
     }
     if (ce >= j) // the packet ends exactly at the last row group's end
         Pe = carry;
