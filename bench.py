@@ -122,9 +122,13 @@ def dist_setup(args):
     dev_index = local % max(ndev, 1)
     torch.cuda.set_device(dev_index)
     coll_dev = torch.device("cuda", dev_index)
-    if world > 1:
+    # WC_DIST_FORCE_PG=1 sets up the process group even for one rank: a
+    # 1-GPU box can then run bench's RCCL code path (barriers, max/sum
+    # reductions, the results all-gather) end to end.
+    if world > 1 or os.environ.get("WC_DIST_FORCE_PG") == "1":
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
         if backend == "nccl":
             dist.init_process_group("nccl", rank=rank, world_size=world,
                                     device_id=torch.device("cuda", dev_index))
@@ -415,7 +419,7 @@ def main():
     # results (RCCL all-gather over xGMI; host tensors for the gloo
     # rehearsal), so every rank holds the whole job's results in packet order.
     gather = None
-    if world > 1 and out.numel() == n:
+    if (world > 1 or wdist._pg_active()) and out.numel() == n:
         src = out.view(torch.int16)
         if coll_dev.type != "cuda":
             src = src.cpu()
@@ -483,7 +487,7 @@ def main():
         if gather is not None:
             line["results_allgather"] = gather
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if wdist._pg_active():
         import torch.distributed as dist
         dist.barrier()
         dist.destroy_process_group()

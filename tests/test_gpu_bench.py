@@ -124,3 +124,22 @@ def test_bench_c5_two_rank_split(gpu):
     assert line["config"]["launches_per_step"] == 2
     assert line["config"]["packets_per_gpu"] == 1 << 21
     assert line["parity"] == {"checked_packets": 2 << 20, "mismatches": 0}
+
+
+def test_bench_rccl_code_path_one_rank(gpu):
+    """bench.py's RCCL (backend "nccl") branch end to end on one GPU: process
+    group on cuda:0, barriers, max/sum reductions and the results all-gather
+    over RCCL -- the path the driver's 2/4/8-GPU runs take, one rank."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(port), WC_DIST_FORCE_PG="1", WC_DIST_BACKEND="nccl")
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "1", "--steps", "5",
+                        "--warmup", "1", "--packets", "65536", "--no-cpu-baseline"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = _last_json(r.stdout)
+    assert line["n_gpus"] == 1 and line["parity"]["mismatches"] == 0
+    assert line["results_allgather"]["ranks_mismatched"] == 0
