@@ -23,7 +23,7 @@ def lib():
                         "-shared", "-o", str(so), str(src)], check=True)
     l = ctypes.CDLL(str(so))
     l.probe_read.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
-                             ctypes.c_void_p, ctypes.c_void_p]
+                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
     return l
 
 
@@ -38,13 +38,14 @@ def main():
     buf = torch.randint(0, 255, (nbytes,), dtype=torch.uint8, device="cuda")
     sink = torch.zeros(64, dtype=torch.int32, device="cuda")
     st = torch.cuda.current_stream()
-    cases = [(64, 4), (16, 4), (8, 4), (4, 4), (2, 4), (1, 4), (64, 2), (4, 2), (1, 2),
-             (64, 8), (4, 8), (1, 8)]
+    cases = [(w, k, sh) for (w, k) in [(64, 4), (16, 4), (8, 4), (4, 4), (4, 2), (8, 2),
+                                       (16, 2), (2, 4)]
+             for sh in (0, 1, 2, 4)]
     t = {c: [] for c in cases}
     for _ in range(args.rounds):
-        for w, k in cases:
+        for w, k, sh in cases:
             fn = lambda: L.probe_read(buf.data_ptr(), nbytes, w, k, sink.data_ptr(),  # noqa
-                                      st.cuda_stream)
+                                      st.cuda_stream, sh)
             assert fn() == 0
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(st)
@@ -52,10 +53,11 @@ def main():
                 fn()
             e1.record(st)
             e1.synchronize()
-            t[(w, k)].append(e0.elapsed_time(e1) / args.iters)
-    for (w, k), ts in t.items():
+            t[(w, k, sh)].append(e0.elapsed_time(e1) / args.iters)
+    for (w, k, sh), ts in t.items():
         med = statistics.median(ts)
-        print(f"W={w:<3} K={k}  {med * 1e3:8.1f} us  {nbytes / med / 1e6:8.1f} GB/s  "
+        print(f"W={w:<3} K={k} shift={16 * sh:<3}B  {med * 1e3:8.1f} us  "
+              f"{nbytes / med / 1e6:8.1f} GB/s  "
               f"{nbytes / med / 1e6 / 80:5.1f}% of 8 TB/s", flush=True)
 
 
