@@ -41,26 +41,18 @@ def host(t: torch.Tensor) -> np.ndarray:
 
 # Ragged kernel paths (wc_cksum_api.cpp plan_ragged, k_cksum_seg): the flat
 # kernel alone; the seg kernel without its grouped path; the grouped path
-# forced for every tile; the walk path forced for every tile at W = 2, 4 and
-# 8 lanes per group (WC_WALK = log2 W | 0x300); and the default per-tile
-# choice.
+# forced for every tile; and the default per-tile choice.
 RAGGED_MODES = {
     "flat": {"WC_SEG": "0"},
     "flat2": {"WC_SEG": "0", "WC_FLAT_PK": "2"},
-    "seg": {"WC_SEG": "1", "WC_GRP_DENSE": "65", "WC_GRP_SPARSE": "65", "WC_WALK": "0"},
-    "grp": {"WC_SEG": "1", "WC_GRP_DENSE": "0", "WC_GRP_SPARSE": "0", "WC_WALK": "0"},
-    "walk2": {"WC_SEG": "1", "WC_WALK": str(1 | 0x300)},
-    "walk4": {"WC_SEG": "1", "WC_WALK": str(2 | 0x300)},
-    "walk8": {"WC_SEG": "1", "WC_WALK": str(3 | 0x300)},
-    "flatwhole": {"WC_SEG": "0", "WC_WALK": str(0x1000)},
-    "segwhole": {"WC_SEG": "1", "WC_GRP_DENSE": "65", "WC_GRP_SPARSE": "65",
-                 "WC_WALK": str(0x1000)},
+    "seg": {"WC_SEG": "1", "WC_GRP_DENSE": "65", "WC_GRP_SPARSE": "65"},
+    "grp": {"WC_SEG": "1", "WC_GRP_DENSE": "0", "WC_GRP_SPARSE": "0"},
     "default": {},
 }
 
 
 def ragged_mode(monkeypatch, mode: str) -> None:
-    for k in ("WC_SEG", "WC_GRP_DENSE", "WC_GRP_SPARSE", "WC_FLAT_PK", "WC_WALK"):
+    for k in ("WC_SEG", "WC_GRP_DENSE", "WC_GRP_SPARSE", "WC_FLAT_PK"):
         monkeypatch.delenv(k, raising=False)
     for k, v in RAGGED_MODES[mode].items():
         monkeypatch.setenv(k, v)

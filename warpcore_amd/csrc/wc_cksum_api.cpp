@@ -110,7 +110,6 @@ struct Config {
     int grp_sparse = 40;           // WC_GRP_SPARSE
     int grp_rows = 4;              // WC_GRP_ROWS
     int flat_pk = 1;               // WC_FLAT_PK: flat kernel chunks per lane slot
-    int walk = 0;                  // WC_WALK: seg kernel walk path (log2 W | A/B bits)
 };
 
 std::mutex g_mu;
@@ -175,7 +174,6 @@ void load_config_locked()
     c.grp_sparse = env_int("WC_GRP_SPARSE", c.grp_sparse);
     c.grp_rows = env_int("WC_GRP_ROWS", c.grp_rows);
     c.flat_pk = env_int("WC_FLAT_PK", c.flat_pk);
-    c.walk = env_int("WC_WALK", c.walk);
     g_cfg = c;
     g_cfg_loaded = true;
 }
@@ -396,7 +394,6 @@ int run(const Device &D, const Config &C, const wc::LaunchArgs &args, const Plan
     a.grp_thr = C.grp_dense | (C.grp_sparse << 8);
     a.grp_rows = C.grp_rows;
     a.flat_pk = C.flat_pk;
-    a.walk = C.walk;
     hipError_t e = p.shape.group == 0 ? wc::launch_flat(a, p.shape.unroll, st)
                                       : wc::launch_cksum(a, p.shape, p.grid, st);
     return hip_err(e);

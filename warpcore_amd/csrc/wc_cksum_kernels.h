@@ -84,9 +84,6 @@ struct LaunchArgs {
     int grp_thr = 65 | (40 << 8);
     int grp_rows = 4; // k_cksum_seg grouped path: rows per ping-pong group (2, 4)
     int flat_pk = 1;  // flat kernel: 16-byte chunks per lane slot (1, or 2 = 32 B per lane)
-    // k_cksum_seg walk path for sparse mixed tiles: log2 lanes per group (0 =
-    // off); bit 8 also dense tiles, bit 9 also uniform tiles (A/B)
-    int walk = 0;
 };
 
 struct Shape {

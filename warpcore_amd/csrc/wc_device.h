@@ -300,22 +300,6 @@ __device__ __forceinline__ void accum_arith(const u32x4 &d, int co, int rs, int 
     }
 }
 
-// Byte-lane sums of the bytes of a chunk at positions [lo, hi) (arithmetic
-// weights): the bytes of a packet's first / last chunk outside it, for the
-// paths that sum chunks whole.
-__device__ __forceinline__ void chunk_range_sums(const u32x4 &d, uint32_t lo, uint32_t hi,
-                                                 uint32_t &E, uint32_t &O)
-{
-    const uint32_t kb = (1u << hi) - (1u << lo);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const uint32_t w = expand_nibble(kb, j), x = pick_dword(d, j);
-        E = dot4(x, w & kEvenB, E);
-        O = dot4(x, w & kOddB, O);
-    }
-}
-
-
 // One chunk of the strided kernel: chunks strictly inside the summed range
 // (and past the header) take the full-weight path; the wave takes the masked
 // path only when one of its lanes holds a head / tail / header chunk of its

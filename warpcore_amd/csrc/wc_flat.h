@@ -120,7 +120,7 @@ __device__ __forceinline__ void flat_issue(FlatRows<UN, PK> &R, FlatLds<UN> &L,
     }
 }
 
-template <int UN, int KIND, bool ARITH = false, int PK = 1, bool WHOLE = false>
+template <int UN, int KIND, bool ARITH = false, int PK = 1>
 __device__ __forceinline__ void flat_accum(const FlatRows<UN, PK> &R, FlatLds<UN> &L,
                                            const WeightLut *M, uint32_t g0,
                                            int lane, uint32_t cp, uint32_t ce,
@@ -136,9 +136,7 @@ __device__ __forceinline__ void flat_accum(const FlatRows<UN, PK> &R, FlatLds<UN
 #pragma unroll
         for (int j = 0; j < PK; ++j) {
             const int co = (int)(16u * ((uint32_t)PK * q + (uint32_t)j) - rel);
-            if constexpr (WHOLE)
-                accum_full(R.d[u][j], E, O);
-            else if constexpr (ARITH)
+            if constexpr (ARITH)
                 accum_arith<KIND>(R.d[u][j], co, (int)((info >> 16) & 0xFFu),
                                   (int)(info & 0xFFFFu), (info >> 24) & 1u, E, O);
             else
@@ -274,15 +272,13 @@ __device__ __forceinline__ uint16_t lane_hdr_cksum(uint64_t a, uint32_t hl,
 // reference accumulator (in_cksum.c:140-167 / 107-120, mod 2^32) -- the
 // caller folds it.  `after_first_issue` runs once the tile's first row group
 // is in flight (the caller's next-tile prefetch goes there).
-template <int UN, int KIND, bool NT, bool NOLOAD, bool ARITH, class F, int PK = 1,
-          bool WHOLE = false>
+template <int UN, int KIND, bool NT, bool NOLOAD, bool ARITH, class F, int PK = 1>
 __device__ __forceinline__ uint32_t flat_tile_sum(FlatLds<UN> &L, const WeightLut *lut,
                                                   int lane, uint64_t a, uint32_t len,
                                                   bool valid, const PseudoHdr &ph,
                                                   F &&after_first_issue)
 {
     static_assert(PK == 1 || !NOLOAD, "diagnostic build: one chunk per slot");
-    static_assert(!WHOLE || (PK == 1 && KIND == WC_KIND_IP), "whole chunks: ip_cksum ranges");
     const uint32_t s = (uint32_t)(a & 15u);
     const uint32_t span = KIND == WC_KIND_PAYLOAD ? max(len, 20u) : len;
     const uint32_t nch = valid ? (s + span + 15u) >> 4 : 0u;
@@ -327,37 +323,23 @@ __device__ __forceinline__ uint32_t flat_tile_sum(FlatLds<UN> &L, const WeightLu
             flat_issue<UN, NT, NOLOAD, PK, KIND>(B, L, j + kGrp, lane, cp, ce, rank, last_rank,
                                                  total);
             __builtin_amdgcn_sched_barrier(0);
-            flat_accum<UN, KIND, ARITH, PK, WHOLE>(A, L, lut, j, lane, cp, ce, total, acc);
+            flat_accum<UN, KIND, ARITH, PK>(A, L, lut, j, lane, cp, ce, total, acc);
             __builtin_amdgcn_sched_barrier(0);
             flat_issue<UN, NT, NOLOAD, PK, KIND>(A, L, j + 2 * kGrp, lane, cp, ce, rank,
                                                  last_rank, total);
             __builtin_amdgcn_sched_barrier(0);
-            flat_accum<UN, KIND, ARITH, PK, WHOLE>(B, L, lut, j + kGrp, lane, cp, ce, total, acc);
+            flat_accum<UN, KIND, ARITH, PK>(B, L, lut, j + kGrp, lane, cp, ce, total, acc);
             __builtin_amdgcn_sched_barrier(0);
         }
         if (j + kGrp < total) {
             flat_issue<UN, NT, NOLOAD, PK, KIND>(B, L, j + kGrp, lane, cp, ce, rank, last_rank,
                                                  total);
             __builtin_amdgcn_sched_barrier(0);
-            flat_accum<UN, KIND, ARITH, PK, WHOLE>(A, L, lut, j, lane, cp, ce, total, acc);
+            flat_accum<UN, KIND, ARITH, PK>(A, L, lut, j, lane, cp, ce, total, acc);
             __builtin_amdgcn_sched_barrier(0);
-            flat_accum<UN, KIND, ARITH, PK, WHOLE>(B, L, lut, j + kGrp, lane, cp, ce, total, acc);
+            flat_accum<UN, KIND, ARITH, PK>(B, L, lut, j + kGrp, lane, cp, ce, total, acc);
         } else {
-            flat_accum<UN, KIND, ARITH, PK, WHOLE>(A, L, lut, j, lane, cp, ce, total, acc);
-        }
-    }
-    if constexpr (WHOLE) {
-        // Chunks were summed whole: take out the bytes [0, s) of the
-        // packet's first chunk and [e, 16) of its last (just streamed: cache
-        // hits), once per packet instead of masking every chunk.
-        if (nch) {
-            const uint64_t c0 = a & ~15ull;
-            const u32x4 hc = load_chunk<false>(c0), tc = load_chunk<false>(c0 + 16ull * (nch - 1u));
-            const uint32_t e = ((s + len - 1u) & 15u) + 1u;
-            uint32_t Ej = 0, Oj = 0;
-            chunk_range_sums(hc, 0u, s, Ej, Oj);
-            chunk_range_sums(tc, e, 16u, Ej, Oj);
-            acc -= combine(Ej, Oj, (s & 1u) != 0u);
+            flat_accum<UN, KIND, ARITH, PK>(A, L, lut, j, lane, cp, ce, total, acc);
         }
     }
     return acc;
@@ -367,7 +349,7 @@ __device__ __forceinline__ uint32_t flat_tile_sum(FlatLds<UN> &L, const WeightLu
 // payload_as_ip runs as ip_cksum over [8, len) with per-packet terms (the
 // range start 8 rides in the descriptor's hl field); any other tile takes
 // the generic payload accumulate.  Tile-uniform choice.
-template <int UN, bool NT, bool ARITH, class F, int PK = 1, bool WHOLE = false>
+template <int UN, bool NT, bool ARITH, class F, int PK = 1>
 __device__ __forceinline__ uint32_t flat_tile_sum_payload(FlatLds<UN> &L, const WeightLut *lut,
                                                           int lane, uint64_t a, uint32_t len,
                                                           bool valid, const PseudoHdr &ph,
@@ -375,13 +357,6 @@ __device__ __forceinline__ uint32_t flat_tile_sum_payload(FlatLds<UN> &L, const 
 {
     uint32_t extra = 0;
     const bool fast = !valid || payload_as_ip(hdr, a, len, ph, extra);
-    if constexpr (WHOLE && PK == 1) {
-        // the range [a + 8, a + len) as an ip_cksum packet (same parity)
-        if (!__ballot(!fast))
-            return flat_tile_sum<UN, WC_KIND_IP, NT, false, ARITH, F, PK, true>(
-                L, lut, lane, a + 8u, valid ? len - 8u : 0u, valid, PseudoHdr{0u, 0u, extra},
-                (F &&)after_first_issue);
-    }
     if (!__ballot(!fast))
         return flat_tile_sum<UN, WC_KIND_IP, NT, false, ARITH, F, PK>(
             L, lut, lane, a, len, valid, PseudoHdr{8u, 0u, extra}, (F &&)after_first_issue);

@@ -5,7 +5,7 @@
 
 namespace wc {
 
-template <int UN, int KIND, bool NT, bool HDR, bool NOLOAD = false, int PK = 1, bool WHOLE = false>
+template <int UN, int KIND, bool NT, bool HDR, bool NOLOAD = false, int PK = 1>
 __global__ void __launch_bounds__(256)
 k_cksum_flat(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
              const uint16_t *__restrict__ lens, uint64_t n,
@@ -60,12 +60,11 @@ k_cksum_flat(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
         };
         uint32_t acc;
         if constexpr (KIND == WC_KIND_PAYLOAD && !NOLOAD)
-            acc = flat_tile_sum_payload<UN, NT, false, decltype(next_hdr) &, PK, WHOLE>(
+            acc = flat_tile_sum_payload<UN, NT, false, decltype(next_hdr) &, PK>(
                 L, &lut, lane, a, len, valid, ph, hdr, next_hdr);
         else
-            acc = flat_tile_sum<UN, KIND, NT, NOLOAD, false, decltype(next_hdr) &, PK,
-                                WHOLE && KIND == WC_KIND_IP>(L, &lut, lane, a, len, valid, ph,
-                                                             next_hdr);
+            acc = flat_tile_sum<UN, KIND, NT, NOLOAD, false, decltype(next_hdr) &, PK>(
+                L, &lut, lane, a, len, valid, ph, next_hdr);
 
         const uint16_t r = fold_not(acc);
         if (valid && out)
@@ -94,10 +93,7 @@ static hipError_t launch_flat_un(const LaunchArgs &a, hipStream_t st)
     const uint8_t *b = (const uint8_t *)a.base;
     unsigned long long *bad = (unsigned long long *)a.bad;
 #define WC_FLAT(K, N, H)                                                       \
-    if (a.walk & 0x1000)                                                       \
-        hipLaunchKernelGGL((k_cksum_flat<UN, K, N, H, false, 1, true>), dim3(grid), dim3(256), \
-                           0, st, b, a.offs, a.lens, a.n, a.out, bad, a.out_hdr); \
-    else if (a.flat_pk == 2)                                                   \
+    if (a.flat_pk == 2)                                                        \
         hipLaunchKernelGGL((k_cksum_flat<UN, K, N, H, false, 2>), dim3(grid), dim3(256), 0, \
                            st, b, a.offs, a.lens, a.n, a.out, bad, a.out_hdr); \
     else                                                                       \

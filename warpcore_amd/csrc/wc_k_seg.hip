@@ -532,260 +532,6 @@ __device__ __forceinline__ uint16_t grp_tile(GrpLds &L, int lane, uint64_t a, ui
     return (uint16_t)L.res[lane];
 }
 
-// ---------------------------------------------------------------------------
-// Ragged batches, sparse tiles of mixed sizes: the "walk" path.
-//
-// A netmap RX ring of mixed sizes (one packet of any length per 2048-B slot,
-// backend_netmap.c:379-391) is neither dense (seg) nor uniform (grouped).
-// The flat path deals its chunks to lanes one 64-chunk row at a time, and
-// pays an owner lookup and a segmented prefix scan per row: ~77 VALU per KiB,
-// issue-bound at 55-59 % of HBM peak (profiles/ab_r02_zslots_classgrp.log).
-// The walk path removes both:
-//   * the tile's chunks are numbered 0..T-1 in packet order (as in flat), and
-//     the wave's G = 64 / W lane groups each take one contiguous range of
-//     Q = ceil(T / G) positions (rounded up to W): every group does the same
-//     number of steps whatever the length mix;
-//   * lane j of a group handles positions j, j + W, j + 2 W, ... of its range,
-//     so each step of a group reads W consecutive chunks of one packet;
-//   * each lane WALKS its packets: it holds its current packet and the next
-//     one's descriptor (prefetched from LDS), so a chunk's address is one
-//     subtraction and a shift -- no owner lookup, no scan;
-//   * chunks are summed WHOLE (8 dot4, no masks) into exact byte-lane sums
-//     (E, O) of the lane's current packet, handed in with one ds_write when
-//     the lane moves on -- no atomics: lane j of the packet's home group (the
-//     group whose range holds its first position) writes slot part[r][j], a
-//     lane whose FIRST packet started in an earlier group writes its own
-//     carry slot; the packet's lane adds its W slots and the carry slots of
-//     the groups its positions reach into;
-//   * the bytes of a packet's first and last chunk outside the packet (at most
-//     15 + 15) are taken out once per packet by the packet's own lane at the
-//     end of the tile, from two re-loads of lines just streamed.
-// A lane past its range re-reads its last chunk into a sink (rank 64).
-// payload_cksum runs as ip_cksum over [a + 8, a + len) plus the per-packet
-// terms of payload_as_ip (wc_flat.h); a tile with an IPv4 header with
-// options, a malformed one or a packet shorter than its header takes the
-// generic flat path.  The sums are exact (E, O), so the reference's uint32
-// wrap (in_cksum.c:157) is reproduced for any start alignment.
-
-constexpr uint32_t kWalkMaxW = 8;
-
-struct WalkLds {
-    u32x4 desc[65]; // rank r: chunk base lo / hi, first position, chunk count;
-                    // desc[nr].z = T (sentinel)
-    // (E, O) partial sums: [r * W + j] home-group slots, [64 W + lane] carry
-    // slots (64 W <= 512)
-    uint2 part[64 * kWalkMaxW + 64];
-};
-
-template <int UNW>
-struct WalkRows {
-    u32x4 d[UNW];
-    uint32_t r[UNW]; // rank the chunk is summed into (64: sink)
-};
-
-struct WalkIssue {
-    uint32_t q, qend, r, cp, end;
-    uint64_t cb, addr;
-    u32x4 nx; // descriptor of rank r + 1
-};
-
-// The walk (branches) runs for all UNW steps first, the loads follow as
-// straight-line code: a load inside the walk's control flow was tail-
-// duplicated by hipcc into both arms, and the phi copy of its result waited
-// for it (vmcnt(0) on every step).
-template <int UNW, bool NT>
-__device__ __forceinline__ void walk_issue(WalkRows<UNW> &R, WalkIssue &I, const WalkLds &L,
-                                           uint32_t W)
-{
-    uint64_t addr[UNW];
-#pragma unroll
-    for (int u = 0; u < UNW; ++u) {
-        const bool live = I.q < I.qend;
-        if (live && I.q >= I.end) {
-            do { // on to the next packet (ranks hold contiguous positions)
-                ++I.r;
-                I.cb = (uint64_t)I.nx.x | ((uint64_t)I.nx.y << 32);
-                I.cp = I.nx.z;
-                I.end = I.nx.z + I.nx.w;
-                I.nx = L.desc[I.r + 1u];
-            } while (I.q >= I.end);
-        }
-        I.addr = live ? I.cb + 16ull * (I.q - I.cp) : I.addr;
-        addr[u] = I.addr;
-        R.r[u] = live ? I.r : 64u;
-        I.q += W;
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int u = 0; u < UNW; ++u)
-        R.d[u] = load_chunk<NT>(addr[u]);
-}
-
-struct WalkAcc {
-    uint32_t r, E, O;
-    uint32_t slot; // where the current packet's sums go
-    uint32_t wlog, j;
-};
-
-__device__ __forceinline__ void walk_flush(WalkAcc &S, WalkLds &L)
-{
-    if (S.r != 64u)
-        L.part[S.slot] = uint2{S.E, S.O};
-}
-
-template <int UNW>
-__device__ __forceinline__ void walk_accum(const WalkRows<UNW> &R, WalkAcc &S, WalkLds &L)
-{
-#pragma unroll
-    for (int u = 0; u < UNW; ++u) {
-        if (R.r[u] != S.r) { // the lane moved on: hand in the old packet's sums
-            walk_flush(S, L);
-            S.E = S.O = 0u;
-            S.r = R.r[u];
-            S.slot = (S.r << S.wlog) + S.j; // the new packet starts in this range
-        }
-        accum_full(R.d[u], S.E, S.O);
-    }
-}
-
-// One sparse tile.  wlog = log2 W (lanes per group, W <= 8).  Returns this
-// lane's packet's checksum, or done = false (payload_cksum tile that needs the
-// generic path).
-template <int UNW, int KIND, bool NT>
-__device__ __forceinline__ uint16_t walk_tile(WalkLds &L, int lane, uint64_t a, uint32_t len,
-                                              bool valid, uint32_t wlog, bool &done)
-{
-    constexpr bool PL = KIND == WC_KIND_PAYLOAD;
-    HdrRaw hdr{};
-    if constexpr (PL)
-        hdr = load_hdr(a);
-    // Summed range [b0, a + len): the whole packet, or [a + 8, a + len).
-    const uint32_t rs = PL ? 8u : 0u;
-    const uint64_t b0 = a + rs;
-    const uint32_t lr = valid && len > rs ? len - rs : 0u;
-    const uint32_t s = (uint32_t)(b0 & 15u);
-    const uint32_t nch = lr ? (s + lr + 15u) >> 4 : 0u;
-    const uint32_t ce = wave_incl_sum(nch), cp = ce - nch;
-    const uint32_t T = lane_u32(ce, 63);
-    const uint64_t ne = __ballot(nch != 0u);
-    const uint32_t rank = mbcnt64(ne);
-    const uint32_t nr = (uint32_t)__builtin_popcountll(ne);
-    const uint64_t cb = b0 & ~15ull;
-    const uint32_t W = 1u << wlog, G = 64u >> wlog;
-    if (nch)
-        L.desc[rank] = u32x4{(uint32_t)cb, (uint32_t)(cb >> 32), cp, nch};
-    if (lane == 0)
-        L.desc[nr] = u32x4{0u, 0u, T, 0u};
-    {
-        u32x4 *z = reinterpret_cast<u32x4 *>(L.part);
-        const uint32_t n16 = (64u * W + 64u) / 2u;
-        for (uint32_t i = (uint32_t)lane; i < n16; i += 64u)
-            z[i] = u32x4{0u, 0u, 0u, 0u};
-    }
-    wave_order();
-
-    const uint32_t Q = (((T + G - 1u) >> (6u - wlog)) + W - 1u) & ~(W - 1u);
-    const uint32_t steps = Q >> wlog;
-    const uint32_t j = (uint32_t)lane & (W - 1u);
-    const uint32_t g0 = ((uint32_t)lane >> wlog) * Q; // the group's first position
-    WalkIssue I;
-    I.q = g0 + j;
-    I.qend = min(g0 + Q, T);
-    // Rank holding the lane's first position (binary search over the ranks'
-    // first positions).
-    const uint32_t qs = min(I.q, T - 1u);
-    uint32_t r0 = 0;
-#pragma unroll
-    for (uint32_t k = 32; k; k >>= 1)
-        if (r0 + k < nr && L.desc[r0 + k].z <= qs)
-            r0 += k;
-    const u32x4 cur = L.desc[r0];
-    I.r = r0;
-    I.cb = (uint64_t)cur.x | ((uint64_t)cur.y << 32);
-    I.cp = cur.z;
-    I.end = cur.z + cur.w;
-    I.addr = I.cb;
-    I.nx = L.desc[r0 + 1u];
-
-    WalkRows<UNW> A, B;
-    if (T != 0u)
-        walk_issue<UNW, NT>(A, I, L, W);
-    uint32_t extra = 0;
-    if constexpr (PL) {
-        PseudoHdr ph{0u, 1u, 0u};
-        if (valid)
-            ph = hdr_pseudo(hdr, a);
-        const bool fast = !valid || payload_as_ip(hdr, a, len, ph, extra);
-        if (__ballot(!fast)) {
-            done = false;
-            return 0;
-        }
-    }
-    done = true;
-    if (T != 0u) {
-        __builtin_amdgcn_sched_barrier(0);
-        // A first packet that started in an earlier group goes to the
-        // lane's carry slot.
-        WalkAcc S{r0, 0u, 0u, cur.z < g0 ? 64u * W + (uint32_t)lane : (r0 << wlog) + j, wlog, j};
-        uint32_t k = 0;
-        for (; k + 2u * UNW < steps; k += 2u * UNW) {
-            walk_issue<UNW, NT>(B, I, L, W);
-            __builtin_amdgcn_sched_barrier(0);
-            walk_accum<UNW>(A, S, L);
-            __builtin_amdgcn_sched_barrier(0);
-            walk_issue<UNW, NT>(A, I, L, W);
-            __builtin_amdgcn_sched_barrier(0);
-            walk_accum<UNW>(B, S, L);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        if (k + UNW < steps) {
-            walk_issue<UNW, NT>(B, I, L, W);
-            __builtin_amdgcn_sched_barrier(0);
-            walk_accum<UNW>(A, S, L);
-            __builtin_amdgcn_sched_barrier(0);
-            walk_accum<UNW>(B, S, L);
-        } else {
-            walk_accum<UNW>(A, S, L);
-        }
-        walk_flush(S, L);
-        wave_order();
-    }
-    uint32_t x = extra;
-    if (nch) {
-        // The packet's first and last chunk (just streamed: cache hits), for
-        // the bytes [0, s) and [e, 16) that are not the packet's.
-        const u32x4 hc = load_chunk<false>(cb), tc = load_chunk<false>(cb + 16ull * (nch - 1u));
-        uint32_t E = 0, O = 0;
-        for (uint32_t i = 0; i < W; ++i) {
-            const uint2 p = L.part[(rank << wlog) + i];
-            E += p.x;
-            O += p.y;
-        }
-        // Carry slots of the later groups the packet reaches into: groups
-        // h + 1 .. (cp + nch - 1) / Q, h = cp / Q.
-        const float rq = 1.0f / (float)Q;
-        const uint32_t last = cp + nch - 1u;
-        uint32_t h = (uint32_t)((float)cp * rq);
-        h -= h * Q > cp ? 1u : 0u;
-        h += (h + 1u) * Q <= cp ? 1u : 0u;
-        uint32_t gi = h + 1u;
-        for (uint32_t gq = gi * Q; gq <= last; gq += Q, ++gi) {
-            const uint32_t base = 64u * W + (gi << wlog);
-            for (uint32_t i = 0; i < W; ++i) {
-                const uint2 p = L.part[base + i];
-                E += p.x;
-                O += p.y;
-            }
-        }
-        const uint32_t e = ((s + lr - 1u) & 15u) + 1u;
-        uint32_t Ej = 0, Oj = 0;
-        chunk_range_sums(hc, 0u, s, Ej, Oj);
-        chunk_range_sums(tc, e, 16u, Ej, Oj);
-        x += combine(E - Ej, O - Oj, (s & 1u) != 0u);
-    }
-    return fold_not(x);
-}
-
 // Dense-tile test (wave-uniform): every valid packet non-empty, starts and
 // ends non-decreasing, gaps below 4 KiB, and the range at most 9/8 of the
 // tile's bytes + 2 KiB.  Sets the range [A0, A0 + 16 T).
@@ -822,13 +568,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UNS >=
 k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
             const uint16_t *__restrict__ lens, uint64_t n, uint16_t *__restrict__ out,
             unsigned long long *__restrict__ bad, int grp_thr, int variant, uint64_t stride,
-            uint32_t slen, uint16_t *__restrict__ out_hdr, int walk)
+            uint32_t slen, uint16_t *__restrict__ out_hdr)
 {
     static_assert(!HDR || KIND == WC_KIND_PAYLOAD, "header checksum rides on payload");
     union TileLds {
         FlatLds<UN> flat;
         GrpLds grp;
-        WalkLds walk;
         struct {
             u32x4 stage[64 * UNS]; // the row group's chunks
             uint32_t pre[64 * UNS];
@@ -884,14 +629,7 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
         const bool grouped = Rq != 0 && (uint64_t)fill * 64u >= (uint64_t)thr * 1024u * Rq;
         bool done = false;
         uint16_t rh = 0;
-        // Walk path (wlog = log2 lanes per group; 0 = off): sparse tiles that
-        // are not uniform; bit 8 also dense tiles, bit 9 also uniform ones (A/B).
-        const uint32_t wlog = min((uint32_t)walk & 0xFu, 3u);
-        const bool use_walk = !HDR && wlog != 0u &&
-                              (grouped ? (walk & 0x200) != 0 : !dense || (walk & 0x100) != 0);
-        if (use_walk)
-            r = walk_tile<UNG, KIND, NT>(L.walk, lane, a, len, valid, wlog, done);
-        else if (grouped)
+        if (grouped)
             r = grp_tile<UNG, KIND, NT, HDR>(L.grp, lane, a, len, valid, Rq, zero, done, rh);
         else if (dense)
             r = seg_tile<UNS, KIND, NT, HDR>(L.seg.pre, L.seg.stage, lane, a, len, valid, A0, T,
@@ -905,22 +643,12 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
                     ph = hdr_pseudo(hdr, a);
             }
             wave_order();
-            auto noop = [] {};
-            if (walk & 0x1000) { // whole chunks, edge bytes taken out per packet
-                if constexpr (KIND == WC_KIND_PAYLOAD)
-                    r = fold_not(flat_tile_sum_payload<UN, NT, true, decltype(noop) &, 1, true>(
-                        L.flat, nullptr, lane, a, len, valid, ph, hdr, noop));
-                else
-                    r = fold_not(flat_tile_sum<UN, KIND, NT, false, true, decltype(noop) &, 1, true>(
-                        L.flat, nullptr, lane, a, len, valid, ph, noop));
-            } else {
-                if constexpr (KIND == WC_KIND_PAYLOAD)
-                    r = fold_not(flat_tile_sum_payload<UN, NT, true>(L.flat, nullptr, lane, a, len,
-                                                                     valid, ph, hdr, noop));
-                else
-                    r = fold_not(flat_tile_sum<UN, KIND, NT, false, true>(L.flat, nullptr, lane, a,
-                                                                          len, valid, ph, noop));
-            }
+            if constexpr (KIND == WC_KIND_PAYLOAD)
+                r = fold_not(flat_tile_sum_payload<UN, NT, true>(L.flat, nullptr, lane, a, len,
+                                                                 valid, ph, hdr, [] {}));
+            else
+                r = fold_not(flat_tile_sum<UN, KIND, NT, false, true>(L.flat, nullptr, lane, a,
+                                                                      len, valid, ph, [] {}));
             if constexpr (HDR)
                 rh = valid && ph.v4 ? lane_hdr_cksum<NT>(a, ph.hl, nullptr) : (uint16_t)0;
         }
@@ -955,13 +683,13 @@ static hipError_t launch_seg_kernel(const LaunchArgs &a, hipStream_t st)
             return hipErrorInvalidValue;
         hipLaunchKernelGGL((k_cksum_seg<UN, 4, 4, WC_KIND_PAYLOAD, true, false, true>),
                            dim3(grid), dim3(256), 0, st, b, a.offs, a.lens, a.n, a.out, bad,
-                           a.grp_thr, a.variant, a.stride, a.len, a.out_hdr, 0);
+                           a.grp_thr, a.variant, a.stride, a.len, a.out_hdr);
         return hipGetLastError();
     }
 #define WC_SEG_K(K, S)                                                         \
     hipLaunchKernelGGL((k_cksum_seg<UN, US, UG, K, true, S>), dim3(grid), dim3(256), 0, st, \
                        b, a.offs, a.lens, a.n, a.out, bad, a.grp_thr, a.variant, a.stride, \
-                       a.len, nullptr, a.walk)
+                       a.len, nullptr)
 #define WC_SEG(US_, UG_)                                                       \
     {                                                                          \
         constexpr int US = US_, UG = UG_;                                      \
