@@ -122,6 +122,29 @@ def test_strided_sweep(gpu, length):
             np.testing.assert_array_equal(got, want, err_msg=f"stride {stride} start {start}")
 
 
+def test_capped_grid_overlapping_stride(gpu):
+    """More packets than one grid can hold: 2^26 + 1000 overlapping 3000-B
+    packets at stride 16 take the (64,4,1) shape (one packet per wave), whose
+    one-shot grid would need 2^24 + 250 workgroups -- more than gridDim.x *
+    256 threads fits in a uint32 on AMD.  The launcher caps the grid at
+    kMaxGridBlocks and the kernel grid-strides over the rest.
+    The packets around the wrap, both ends and a random sample are checked
+    against the oracle."""
+    n, stride, length = (1 << 26) + 1000, 16, 3000
+    d = torch.empty((n - 1) * stride + length + 64, dtype=torch.uint8, device=gpu)
+    wc.synth_fill(d, 26)
+    got = host(wc.cksum_strided(d, stride, length, n, kind="ip"))
+    wrap = ((1 << 24) - 1) * 4  # first packet of the second grid-stride pass
+    rng = np.random.default_rng(26)
+    idx = np.unique(np.concatenate([np.arange(0, 1000), np.arange(wrap - 1000, wrap + 1000),
+                                    np.arange(n - 2000, n), rng.integers(0, n, 20000)]))
+    buf = d.cpu().numpy()
+    want = c_oracle.cksum_ragged(buf, (idx * stride).astype(np.uint64),
+                                 np.full(idx.size, length, np.uint16), kind=0)
+    np.testing.assert_array_equal(got[idx], want)
+    del d, buf
+
+
 @pytest.mark.parametrize("sseg", ["0", "1", "2"])
 @pytest.mark.parametrize("length", [1, 2, 15, 16, 17, 63, 64, 65, 100, 111, 128, 255, 256, 257,
                                     400, 500, 512, 513, 576, 577, 767, 768, 1472, 1500, 9000])

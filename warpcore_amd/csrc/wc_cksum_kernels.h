@@ -13,6 +13,7 @@
 // WC_SHAPE may request; each is instantiated for ip_cksum (masked and
 // aligned-unmasked) and payload_cksum, with temporal and nontemporal loads.
 #define WC_SHAPE_LIST                                                          \
+    WC_SHAPE(4, 1, 1)                                                          \
     WC_SHAPE(4, 1, 2)                                                          \
     WC_SHAPE(4, 1, 4)                                                          \
     WC_SHAPE(4, 1, 8)                                                          \

@@ -87,8 +87,15 @@ __device__ __forceinline__ uint64_t xcd_block(int variant)
     if (variant & 8)
         return b;
     const uint32_t k = ((uint32_t)variant >> 8) & 0xFFu;
-    const uint32_t span = k == 0 ? 4096u : k >= 31 ? nb : (1u << k);
-    const uint32_t base = b / span * span, m = min(span, nb - base), l = b - base;
+    // Power-of-two spans: shifts, not a division (this runs before any
+    // load of every wave, so it is on the critical path of small batches).
+    uint32_t base = 0, m = nb;
+    if (k < 31) {
+        const uint32_t sh = k == 0 ? 12u : k;
+        base = (b >> sh) << sh;
+        m = min(1u << sh, nb - base);
+    }
+    const uint32_t l = b - base;
     const uint32_t x = l & 7u, q = m >> 3, r = m & 7u;
     return (uint64_t)(base + x * q + min(x, r) + (l >> 3));
 }

@@ -55,17 +55,23 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
         bool valid[U];
         u32x4 d[U][CPL];
 
+        // Strided: packet p0 + u GPW + grp sits GPW * stride after the one
+        // of u - 1 (one 64-bit multiply per wave, not per packet: the
+        // address setup runs before the first load).
+        const uint64_t a_first = (uint64_t)base + p0 * stride;
+        uint64_t a_u = a_first + (uint64_t)grp * stride;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint64_t i = p0 + (uint64_t)u * GPW + grp;
             valid[u] = i < n;
-            const uint64_t ii = valid[u] ? i : p0;
             uint64_t a;
             if constexpr (RAGGED) {
+                const uint64_t ii = valid[u] ? i : p0;
                 a = (uint64_t)base + offs[ii];
                 plen[u] = lens[ii];
             } else {
-                a = (uint64_t)base + ii * stride;
+                a = valid[u] ? a_u : a_first;
+                a_u += (uint64_t)GPW * stride;
                 plen[u] = len;
             }
             // payload_cksum reads the IPv4 header fields up to byte 19 even
@@ -73,7 +79,7 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
             const uint32_t span = KIND == WC_KIND_PAYLOAD ? max(plen[u], 20u) : plen[u];
             s[u] = (int)(a & 15u);
             c0[u] = a & ~15ull;
-            nch[u] = valid[u] ? (uint32_t)((a + span + 15u - c0[u]) >> 4) : 0u;
+            nch[u] = valid[u] ? ((uint32_t)s[u] + span + 15u) >> 4 : 0u;
         }
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -84,6 +90,14 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
                 // zero chunk.
                 d[u][c] = load_chunk<NT>(k < nch[u] ? c0[u] + 16ull * k : zero);
             }
+        // Every load of the iteration is issued before any sum: without the
+        // barrier hipcc hoisted the first packet's dot4s between the loads,
+        // with a vmcnt(0) after the first one, so the (4,1,4) and (8,3,2)
+        // shapes paid two memory latencies per wave (256 B: 86 -> 89-90 % of
+        // HBM peak).  The long shapes keep hipcc's own order, which measured
+        // better for C2 (90.8 vs 90.0 %, profiles/ab_r02_sched_barrier.log).
+        if constexpr (CPL * U < 16)
+            __builtin_amdgcn_sched_barrier(0);
 
 #pragma unroll
         for (int u = 0; u < U; ++u) {
