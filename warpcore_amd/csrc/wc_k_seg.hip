@@ -619,14 +619,32 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
         uint64_t A0 = 0;
         uint32_t T = 0;
         uint16_t r = 0;
-        const bool dense = seg_dense(lane, a, len, valid, nvalid, A0, T);
-        // Uniform tile?  Chunk fill of the grouped path's 1024 R slots.
-        const uint32_t span = grp_span<KIND>(len);
-        const uint32_t nchg = valid ? ((uint32_t)(a & 15u) + span + 15u) >> 4 : 0u;
-        const uint32_t Rq = (wave_max(nchg) + 15u) >> 4;
-        const uint32_t fill = lane_u32(wave_incl_sum(nchg), 63);
+        bool dense;
+        if constexpr (STR) {
+            // Packed strided batch (the planner's precondition: len > 0,
+            // len <= stride <= len + len / 8, < 90 chunks): every tile is
+            // dense, and its range follows from the stride -- no wave
+            // reductions before the first load.
+            dense = true;
+            const uint64_t a0 = (uint64_t)base + tile * 64u * stride;
+            A0 = a0 & ~15ull;
+            T = (uint32_t)((a0 + (uint64_t)(nvalid - 1u) * stride + slen - A0 + 15u) >> 4);
+        } else {
+            dense = seg_dense(lane, a, len, valid, nvalid, A0, T);
+        }
+        // Uniform tile?  Chunk fill of the grouped path's 1024 R slots --
+        // only computed when the threshold for this kind of tile can be met
+        // (dense tiles never take the grouped path by default).
         const uint32_t thr = dense ? (uint32_t)(grp_thr & 0xFF) : (uint32_t)(grp_thr >> 8);
-        const bool grouped = Rq != 0 && (uint64_t)fill * 64u >= (uint64_t)thr * 1024u * Rq;
+        uint32_t Rq = 0;
+        bool grouped = false;
+        if (thr <= 64u) {
+            const uint32_t span = grp_span<KIND>(len);
+            const uint32_t nchg = valid ? ((uint32_t)(a & 15u) + span + 15u) >> 4 : 0u;
+            Rq = (wave_max(nchg) + 15u) >> 4;
+            const uint32_t fill = lane_u32(wave_incl_sum(nchg), 63);
+            grouped = Rq != 0 && (uint64_t)fill * 64u >= (uint64_t)thr * 1024u * Rq;
+        }
         bool done = false;
         uint16_t rh = 0;
         if (grouped)
