@@ -13,6 +13,7 @@ for c in ${CASES:-c4:payload}; do
     case $cfg in
         c2) a="--config c2" ;;
         c4) a="--config c4" ;;
+        zslots) a="--config zslots" ;;
         slot) a="--config c3 --len 1500 --stride 2048 --offset 14" ;;
         rslot) a="--config c3 --len 1500 --stride 2048 --offset 14 --ragged" ;;
         rc2) a="--config c2 --ragged" ;;

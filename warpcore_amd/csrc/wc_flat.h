@@ -268,6 +268,80 @@ __device__ __forceinline__ uint16_t lane_hdr_cksum(uint64_t a, uint32_t hl,
     return fold_not(combine(E, O, s & 1u));
 }
 
+// Per-tile layout of the flat path: slot range [cp, ce) of this lane's
+// packet within the tile, the tile's slot count, and the packet's rank among
+// the tile's non-empty packets.  Slot q's chunk j is the packet's chunk
+// PK (q - cp) + j, at vb + 16 (PK q + j).
+struct FlatTile {
+    uint32_t cp, ce, total, rank, last_rank;
+};
+
+template <int UN, int PK>
+__device__ __forceinline__ FlatTile flat_tile_setup(FlatLds<UN> &L, int lane, uint64_t a,
+                                                    uint32_t len, uint32_t span, bool valid,
+                                                    uint32_t info)
+{
+    const uint32_t s = (uint32_t)(a & 15u);
+    const uint32_t nch = valid ? (s + span + 15u) >> 4 : 0u;
+    const uint32_t nsl = (nch + PK - 1u) / PK; // slots of PK chunks
+    FlatTile t;
+    t.ce = wave_incl_sum(nsl);
+    t.cp = t.ce - nsl;
+    t.total = lane_u32(t.ce, 63);
+    const uint64_t nonempty = __ballot(nch != 0);
+    t.rank = mbcnt64(nonempty);
+    t.last_rank = nonempty ? (uint32_t)__builtin_popcountll(nonempty) - 1u : 0u;
+    const uint64_t vb = (a & ~15ull) - 16ull * PK * t.cp;
+    if (nch != 0)
+        L.desc[t.rank] = FlatDesc{(uint32_t)vb, (uint32_t)(vb >> 32), s + 16u * PK * t.cp, info};
+    // Row marks carry the row's number within the tile; reset them to a
+    // tag no row has so the previous tile's marks can't match.
+#pragma unroll
+    for (int u = 0; u < UN; ++u)
+        L.mark[u][lane] = 0xFFFFFFFFu;
+    wave_order();
+    return t;
+}
+
+// The tile's row groups after the first one (A, already issued): ping-pong
+// A / B (no register copies), group g+1's loads in flight while group g is
+// summed; sched_barrier keeps each issue ahead of the other group's sum.
+// While a third group still holds tile slots; then a tail of one or two
+// groups.  Every issued group is summed: a load left pending at the loop's
+// exit makes hipcc wait vmcnt(0) at the loop head on every iteration
+// (measured in the ISA with a mid-loop exit).
+template <int UN, int KIND, bool NT, bool NOLOAD, bool ARITH, int PK>
+__device__ __forceinline__ void flat_tile_loop(FlatRows<UN, PK> &A, FlatLds<UN> &L,
+                                               const WeightLut *lut, int lane,
+                                               const FlatTile &t, uint32_t &acc)
+{
+    constexpr uint32_t kGrp = 64u * UN;
+    FlatRows<UN, PK> B;
+    uint32_t j = 0;
+    for (; j + 2 * kGrp < t.total; j += 2 * kGrp) {
+        flat_issue<UN, NT, NOLOAD, PK, KIND>(B, L, j + kGrp, lane, t.cp, t.ce, t.rank,
+                                             t.last_rank, t.total);
+        __builtin_amdgcn_sched_barrier(0);
+        flat_accum<UN, KIND, ARITH, PK>(A, L, lut, j, lane, t.cp, t.ce, t.total, acc);
+        __builtin_amdgcn_sched_barrier(0);
+        flat_issue<UN, NT, NOLOAD, PK, KIND>(A, L, j + 2 * kGrp, lane, t.cp, t.ce, t.rank,
+                                             t.last_rank, t.total);
+        __builtin_amdgcn_sched_barrier(0);
+        flat_accum<UN, KIND, ARITH, PK>(B, L, lut, j + kGrp, lane, t.cp, t.ce, t.total, acc);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    if (j + kGrp < t.total) {
+        flat_issue<UN, NT, NOLOAD, PK, KIND>(B, L, j + kGrp, lane, t.cp, t.ce, t.rank,
+                                             t.last_rank, t.total);
+        __builtin_amdgcn_sched_barrier(0);
+        flat_accum<UN, KIND, ARITH, PK>(A, L, lut, j, lane, t.cp, t.ce, t.total, acc);
+        __builtin_amdgcn_sched_barrier(0);
+        flat_accum<UN, KIND, ARITH, PK>(B, L, lut, j + kGrp, lane, t.cp, t.ce, t.total, acc);
+    } else {
+        flat_accum<UN, KIND, ARITH, PK>(A, L, lut, j, lane, t.cp, t.ce, t.total, acc);
+    }
+}
+
 // One 64-packet tile of the flat kernel: returns this lane's packet's exact
 // reference accumulator (in_cksum.c:140-167 / 107-120, mod 2^32) -- the
 // caller folds it.  `after_first_issue` runs once the tile's first row group
@@ -279,69 +353,17 @@ __device__ __forceinline__ uint32_t flat_tile_sum(FlatLds<UN> &L, const WeightLu
                                                   F &&after_first_issue)
 {
     static_assert(PK == 1 || !NOLOAD, "diagnostic build: one chunk per slot");
-    const uint32_t s = (uint32_t)(a & 15u);
     const uint32_t span = KIND == WC_KIND_PAYLOAD ? max(len, 20u) : len;
-    const uint32_t nch = valid ? (s + span + 15u) >> 4 : 0u;
-    const uint32_t nsl = (nch + PK - 1u) / PK; // slots of PK chunks
-
-    // Slot range [cp, ce) of this lane's packet within the tile; rank among
-    // the tile's non-empty packets.  Slot q's chunk j is the packet's chunk
-    // PK (q - cp) + j, at vb + 16 (PK q + j).
-    const uint32_t ce = wave_incl_sum(nsl);
-    const uint32_t cp = ce - nsl;
-    const uint32_t total = lane_u32(ce, 63);
-    const uint64_t nonempty = __ballot(nch != 0);
-    const uint32_t rank = mbcnt64(nonempty);
-    const uint32_t last_rank = nonempty ? (uint32_t)__builtin_popcountll(nonempty) - 1u : 0u;
-    const uint64_t vb = (a & ~15ull) - 16ull * PK * cp;
-    if (nch != 0)
-        L.desc[rank] = FlatDesc{(uint32_t)vb, (uint32_t)(vb >> 32), s + 16u * PK * cp,
-                                len | (ph.hl << 16) | (ph.v4 << 24)};
-    // Row marks carry the row's number within the tile; reset them to a
-    // tag no row has so the previous tile's marks can't match.
-#pragma unroll
-    for (int u = 0; u < UN; ++u)
-        L.mark[u][lane] = 0xFFFFFFFFu;
-    wave_order();
-
+    const FlatTile t = flat_tile_setup<UN, PK>(L, lane, a, len, span, valid,
+                                               len | (ph.hl << 16) | (ph.v4 << 24));
     uint32_t acc = ph.special;
-    constexpr uint32_t kGrp = 64u * UN;
-    FlatRows<UN, PK> A, B;
-    if (total != 0)
-        flat_issue<UN, NT, NOLOAD, PK, KIND>(A, L, 0, lane, cp, ce, rank, last_rank, total);
+    FlatRows<UN, PK> A;
+    if (t.total != 0)
+        flat_issue<UN, NT, NOLOAD, PK, KIND>(A, L, 0, lane, t.cp, t.ce, t.rank, t.last_rank,
+                                             t.total);
     after_first_issue();
-    if (total != 0) {
-        // Ping-pong row groups A / B (no register copies): group g+1's
-        // loads are in flight while group g is summed; sched_barrier keeps
-        // each issue ahead of the other group's sum.
-        // While a third group still holds tile slots; then a tail of one
-        // or two groups.  Every issued group is summed: a load left pending
-        // at the loop's exit makes hipcc wait vmcnt(0) at the loop head on
-        // every iteration (measured in the ISA with a mid-loop exit).
-        uint32_t j = 0;
-        for (; j + 2 * kGrp < total; j += 2 * kGrp) {
-            flat_issue<UN, NT, NOLOAD, PK, KIND>(B, L, j + kGrp, lane, cp, ce, rank, last_rank,
-                                                 total);
-            __builtin_amdgcn_sched_barrier(0);
-            flat_accum<UN, KIND, ARITH, PK>(A, L, lut, j, lane, cp, ce, total, acc);
-            __builtin_amdgcn_sched_barrier(0);
-            flat_issue<UN, NT, NOLOAD, PK, KIND>(A, L, j + 2 * kGrp, lane, cp, ce, rank,
-                                                 last_rank, total);
-            __builtin_amdgcn_sched_barrier(0);
-            flat_accum<UN, KIND, ARITH, PK>(B, L, lut, j + kGrp, lane, cp, ce, total, acc);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        if (j + kGrp < total) {
-            flat_issue<UN, NT, NOLOAD, PK, KIND>(B, L, j + kGrp, lane, cp, ce, rank, last_rank,
-                                                 total);
-            __builtin_amdgcn_sched_barrier(0);
-            flat_accum<UN, KIND, ARITH, PK>(A, L, lut, j, lane, cp, ce, total, acc);
-            __builtin_amdgcn_sched_barrier(0);
-            flat_accum<UN, KIND, ARITH, PK>(B, L, lut, j + kGrp, lane, cp, ce, total, acc);
-        } else {
-            flat_accum<UN, KIND, ARITH, PK>(A, L, lut, j, lane, cp, ce, total, acc);
-        }
-    }
+    if (t.total != 0)
+        flat_tile_loop<UN, KIND, NT, NOLOAD, ARITH, PK>(A, L, lut, lane, t, acc);
     return acc;
 }
 
