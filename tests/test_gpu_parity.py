@@ -91,8 +91,10 @@ def test_golden_vectors_payload(gpu):
 # ---------------------------------------------------------------------------
 # Edge sweeps: lengths x start alignment x stride, both batch layouts.
 
-SWEEP_LENS = list(range(0, 131)) + [255, 256, 257, 511, 575, 576, 577, 1471, 1472,
-                                    1473, 2048, 4095, 8999, 9000, 9001, 65535]
+SWEEP_LENS = list(range(0, 131)) + [255, 256, 257, 511, 575, 576, 577, 784, 785, 880, 900,
+                                    1000, 1008, 1024, 1040, 1100, 1216, 1232, 1250, 1376,
+                                    1392, 1471, 1472, 1473, 1536, 2048, 4095, 8999, 9000,
+                                    9001, 65535]
 
 
 @pytest.mark.parametrize("group,kind", [("icmp", 0), ("ip4hdr", 0), ("udp6", 1), ("udp4", 1)])

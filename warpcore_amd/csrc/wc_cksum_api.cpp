@@ -253,7 +253,7 @@ int ensure_device(Device **out, Config *cfg)
 // ---------------------------------------------------------------------------
 // Planner.
 
-wc::Shape shape_for_chunks(uint32_t nch)
+wc::Shape shape_for_chunks(uint32_t nch, bool full, bool payload, bool aligned)
 {
     // Smallest group covering the packet in one pass, with U packets per
     // group so every lane keeps ~4-18 16-byte loads in flight (tuned on
@@ -278,8 +278,26 @@ wc::Shape shape_for_chunks(uint32_t nch)
         return {8, 6, 1};
     if (nch <= 48)
         return {16, 3, 2};
-    if (nch <= 96)
-        return {16, 6, 4};
+    // 49..96 chunks (784..1536 B): 32-lane groups with 2-4 loads per lane
+    // beat 16 x 6 for ip_cksum (profiles/sweep_r02_wide_shapes.log: C2
+    // 1472 B 88.6-91 -> 93.3-95 %, 1024 B 82 -> 94 %, 2048-B slots at +14
+    // +2..5 points).  Aligned unmasked (FULL) batches and masked ones differ
+    // below 88 chunks.  payload_cksum (more registers per lane) keeps 16-lane
+    // groups, fewer packets per group when aligned
+    // (profiles/sweep_r02_payload_shapes.log: C2 payload 84 -> 92.5 %).
+    if (payload && nch <= 96) {
+        if (aligned)
+            return {16, 6, 2};
+        return nch <= 80 ? wc::Shape{16, 5, 4} : wc::Shape{32, 3, 2};
+    }
+    if (nch <= 56)
+        return full ? wc::Shape{32, 2, 4} : wc::Shape{16, 5, 4};
+    if (nch <= 63)
+        return full ? wc::Shape{32, 2, 2} : wc::Shape{16, 5, 4};
+    if (nch <= 77)
+        return full ? wc::Shape{32, 4, 2} : wc::Shape{32, 3, 2};
+    if (nch <= 87)
+        return full ? wc::Shape{32, 4, 1} : wc::Shape{32, 4, 2};
     if (nch <= 128)
         return {32, 4, 1};
     if (nch <= 256)
@@ -323,9 +341,10 @@ Plan plan_strided(const Device &D, const Config &C, uint64_t base, uint64_t stri
     // Worst-case start phase within a 16-byte chunk over the batch.
     const uint32_t phase = (stride % 16 == 0) ? (uint32_t)(base % 16) : 15u;
     const uint32_t nch = (phase + span + 15u) / 16u;
-    p.shape = C.have_shape ? C.shape : shape_for_chunks(nch);
     p.full = kind == WC_CKSUM_IP && base % 16 == 0 && stride % 16 == 0 &&
              len % 16 == 0 && !(C.variant & 2);
+    p.shape = C.have_shape ? C.shape
+                           : shape_for_chunks(nch, p.full, kind == WC_CKSUM_PAYLOAD, phase == 0);
     p.grid = grid_for(D, C, p.shape, n);
     // Packed (or nearly packed) packets that the group kernel would have to
     // mask: the seg kernel streams their byte range instead (k_cksum_seg<STR>)

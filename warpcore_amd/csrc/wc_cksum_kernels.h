@@ -36,11 +36,22 @@
     WC_SHAPE(16, 1, 8)                                                         \
     WC_SHAPE(16, 2, 4)                                                         \
     WC_SHAPE(16, 3, 4)                                                         \
+    WC_SHAPE(16, 4, 2)                                                         \
+    WC_SHAPE(16, 4, 4)                                                         \
+    WC_SHAPE(16, 5, 2)                                                         \
+    WC_SHAPE(16, 5, 4)                                                         \
     WC_SHAPE(16, 6, 2)                                                         \
     WC_SHAPE(16, 6, 4)                                                         \
+    WC_SHAPE(32, 2, 2)                                                         \
+    WC_SHAPE(32, 2, 4)                                                         \
+    WC_SHAPE(32, 3, 1)                                                         \
+    WC_SHAPE(32, 3, 2)                                                         \
     WC_SHAPE(32, 3, 4)                                                         \
     WC_SHAPE(32, 3, 8)                                                         \
     WC_SHAPE(32, 4, 1)                                                         \
+    WC_SHAPE(32, 4, 2)                                                         \
+    WC_SHAPE(64, 2, 1)                                                         \
+    WC_SHAPE(64, 2, 2)                                                         \
     WC_SHAPE(32, 18, 1)                                                        \
     WC_SHAPE(64, 4, 1)                                                         \
     WC_SHAPE(64, 9, 1)                                                         \
