@@ -267,8 +267,10 @@ wc::Shape shape_for_chunks(uint32_t nch, bool full, bool payload, bool aligned)
     // 9..24 chunks: 8 lanes x 3 chunks, two packets per group -- fewer dead
     // lane slots than 16 x 2 (tools/sweep_mid.sh: 256 B 78.7 -> 84.1 %,
     // 200 B 55 -> 67.5 %, 256 B at +14 50 -> 60 % of HBM peak)
-    if (nch <= 24)
+    if (nch <= 16 || (nch <= 24 && !full))
         return {8, 3, 2};
+    // aligned unmasked 17..30 chunks: 16 x 2 x 4 (320 B 80.8 -> 85.4 %,
+    // profiles/sweep_r02_small_shapes.log)
     if (nch <= 30)
         return {16, 2, 4};
     // ~512 B: 8 lanes x 6 chunks, one packet per group (85 -> 90.8 % packed,
@@ -276,8 +278,10 @@ wc::Shape shape_for_chunks(uint32_t nch, bool full, bool payload, bool aligned)
     // (profiles/sweep_r01_mid_shapes.log)
     if (nch <= 34)
         return {8, 6, 1};
+    // 35..48 chunks: one packet per 16-lane group when aligned unmasked
+    // (704 B 90.5 -> 93.6 %, 576 B 90.7 -> 91.2 %)
     if (nch <= 48)
-        return {16, 3, 2};
+        return full ? wc::Shape{16, 3, 1} : wc::Shape{16, 3, 2};
     // 49..96 chunks (784..1536 B): 32-lane groups with 2-4 loads per lane
     // beat 16 x 6 for ip_cksum (profiles/sweep_r02_wide_shapes.log: C2
     // 1472 B 88.6-91 -> 93.3-95 %, 1024 B 82 -> 94 %, 2048-B slots at +14

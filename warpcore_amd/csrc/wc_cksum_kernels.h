@@ -29,6 +29,11 @@
     WC_SHAPE(8, 6, 1)                                                          \
     WC_SHAPE(16, 3, 2)                                                         \
     WC_SHAPE(16, 1, 2)                                                         \
+    WC_SHAPE(16, 2, 2)                                                         \
+    WC_SHAPE(16, 3, 1)                                                         \
+    WC_SHAPE(32, 1, 2)                                                         \
+    WC_SHAPE(32, 1, 4)                                                         \
+    WC_SHAPE(32, 2, 1)                                                         \
     WC_SHAPE(4, 1, 16)                                                         \
     WC_SHAPE(8, 1, 4)                                                          \
     WC_SHAPE(8, 1, 8)                                                          \
