@@ -64,7 +64,7 @@ def parse():
                     help="total CPU-baseline time budget (all-thread + 1-core trials)")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="threads for the all-core CPU baseline (default: the box's share)")
-    ap.add_argument("--warmup-seconds", type=float, default=0.3,
+    ap.add_argument("--warmup-seconds", type=float, default=1.0,
                     help="keep warming up (untimed) until this long has passed, so the "
                          "GPU clock has ramped from idle before the timed steps")
     ap.add_argument("--no-cpu-baseline", action="store_true")
