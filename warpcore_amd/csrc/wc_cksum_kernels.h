@@ -66,6 +66,8 @@
 // nontemporal loads).
 #define WC_RAGGED_SHAPE_LIST                                                   \
     WC_SHAPE(16, 2, 2)                                                         \
+    WC_SHAPE(32, 4, 1)                                                         \
+    WC_SHAPE(32, 3, 2)                                                         \
     WC_SHAPE(32, 2, 1)                                                         \
     WC_SHAPE(64, 2, 1)                                                         \
     WC_SHAPE(64, 4, 1)                                                         \
