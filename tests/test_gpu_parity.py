@@ -124,6 +124,32 @@ def test_strided_sweep(gpu, length):
             np.testing.assert_array_equal(got, want, err_msg=f"stride {stride} start {start}")
 
 
+# The planner's tuned shapes for the configurations the bench quotes
+# (wc_cksum_api.cpp shape_for_chunks).  A regression
+# here moves the headline, so it is pinned.
+PLANNED = [
+    # base, stride, len, kind, (group, chunks per lane, packets per group)
+    (0, 1472, 1472, "ip", (32, 4, 1)),        # C2
+    (0, 1472, 1472, "payload", (16, 6, 2)),   # C2 as payload_cksum
+    (14, 2048, 1500, "ip", (32, 4, 1)),       # netmap slots, strided
+    (14, 2048, 1500, "payload", (32, 3, 2)),
+    (0, 1024, 1024, "ip", (32, 4, 2)),
+    (0, 64, 64, "ip", (4, 1, 4)),             # C3 64 B
+    (0, 256, 256, "ip", (8, 3, 2)),
+    (0, 576, 576, "ip", (16, 3, 1)),
+    (0, 9000, 9000, "ip", (32, 18, 1)),
+]
+
+
+@pytest.mark.parametrize("base,stride,length,kind,shape", PLANNED)
+def test_planner_shapes(gpu, monkeypatch, base, stride, length, kind, shape):
+    for k in ("WC_SHAPE", "WC_STRIDED_SEG", "WC_VARIANT"):
+        monkeypatch.delenv(k, raising=False)
+    wc.reload_config()
+    p = wc.plan_strided(0x100000000 + base, stride, length, 1 << 20, kind=kind)
+    assert (p["group"], p["chunks_per_lane"], p["unroll"]) == shape
+
+
 def test_capped_grid_overlapping_stride(gpu):
     """More packets than one grid can hold: 2^26 + 1000 overlapping 3000-B
     packets at stride 16 take the (64,4,1) shape (one packet per wave), whose
