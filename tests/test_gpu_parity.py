@@ -52,7 +52,7 @@ RAGGED_MODES = {
 
 
 def ragged_mode(monkeypatch, mode: str) -> None:
-    for k in ("WC_SEG", "WC_GRP_DENSE", "WC_GRP_SPARSE", "WC_FLAT_PK"):
+    for k in ("WC_SEG", "WC_GRP_DENSE", "WC_GRP_SPARSE", "WC_FLAT_PK", "WC_VARIANT"):
         monkeypatch.delenv(k, raising=False)
     for k, v in RAGGED_MODES[mode].items():
         monkeypatch.setenv(k, v)

@@ -114,6 +114,22 @@ __device__ __forceinline__ u32x4 load_chunk(uint64_t addr)
         return *p;
 }
 
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+// V += the dword's two little-endian 16-bit words (v_dot2_u32_u16): the sum
+// of the words at even addresses of a 16-byte-aligned chunk.
+__device__ __forceinline__ uint32_t wsum(uint32_t x, uint32_t acc)
+{
+    return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, x), u16x2{1, 1}, acc, false);
+}
+
+// 0xFF in the bytes of dword j that are among the first q bytes of a chunk.
+__device__ __forceinline__ uint32_t head_mask(uint32_t q, int j)
+{
+    const uint32_t nb = min(q - min(q, 4u * j), 4u);
+    return nb >= 4u ? 0xFFFFFFFFu : ((1u << (8u * nb)) - 1u);
+}
+
 // in_cksum.c:74-80 -- two end-around folds always suffice for a uint32.
 __device__ __forceinline__ uint16_t fold_not(uint32_t s)
 {

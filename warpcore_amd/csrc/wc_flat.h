@@ -48,6 +48,8 @@ struct FlatLds {
     FlatDesc desc[64];
     uint32_t mark[UN][64]; // run-start tags, one array per row of a group
     uint32_t pre[64 * UN]; // inclusive prefix sums of the group's chunk sums
+    u32x4 pm[17];          // VSUM byte masks: 0xFF in bytes [0, k)
+    u32x4 nm[17];          //                  0xFF in bytes [k, 16)
 };
 
 // Intra-wave LDS hand-offs need no fence: one wave's LDS instructions execute
@@ -120,18 +122,35 @@ __device__ __forceinline__ void flat_issue(FlatRows<UN, PK> &R, FlatLds<UN> &L,
     }
 }
 
-template <int UN, int KIND, bool ARITH = false, int PK = 1>
+// VSUM (ip_cksum ranges, one chunk per slot): each chunk contributes V =
+// the sum of its little-endian words at even addresses (4 v_dot2 of the
+// masked dwords; masks from the pm / nm tables, one v_and3 per dword), not
+// the exact byte-lane pair (E, O) -- half the VALU per chunk.  For an even
+// start V is the reference's accumulator; for an odd one the caller folds
+// rotl32(V, 8) instead, bit-exact by the residue argument of the seg path
+// (wc_k_seg.hip).
+template <int UN, int KIND, bool ARITH = false, int PK = 1, bool VSUM = false>
 __device__ __forceinline__ void flat_accum(const FlatRows<UN, PK> &R, FlatLds<UN> &L,
                                            const WeightLut *M, uint32_t g0,
                                            int lane, uint32_t cp, uint32_t ce,
                                            uint32_t total, uint32_t &acc)
 {
+    static_assert(!VSUM || (PK == 1 && KIND == WC_KIND_IP), "VSUM: ip_cksum, one chunk a slot");
     uint32_t P[UN];
 #pragma unroll
     for (int u = 0; u < UN; ++u) {
         const uint32_t q = g0 + 64u * u + (uint32_t)lane;
         const FlatDesc &g = L.desc[R.own[u]];
         const uint32_t rel = g.rel, info = g.info;
+        if constexpr (VSUM) {
+            const int co = (int)(16u * q - rel);
+            const int rs = (int)((info >> 16) & 0xFFu), re = (int)(info & 0xFFFFu);
+            const int lo = min(max(rs - co, 0), 16), hi = min(max(re - co, 0), 16);
+            const u32x4 x = R.d[u][0] & L.pm[hi] & L.nm[lo];
+            const uint32_t V = wsum(x.w, wsum(x.z, wsum(x.y, wsum(x.x, 0u))));
+            P[u] = q < total ? V : 0u;
+            continue;
+        }
         uint32_t E = 0, O = 0;
 #pragma unroll
         for (int j = 0; j < PK; ++j) {
@@ -276,11 +295,21 @@ struct FlatTile {
     uint32_t cp, ce, total, rank, last_rank;
 };
 
-template <int UN, int PK>
+template <int UN, int PK, bool VSUM = false>
 __device__ __forceinline__ FlatTile flat_tile_setup(FlatLds<UN> &L, int lane, uint64_t a,
                                                     uint32_t len, uint32_t span, bool valid,
                                                     uint32_t info)
 {
+    if constexpr (VSUM) {
+        if (lane < 17) {
+            const uint32_t k = (uint32_t)lane;
+            L.pm[k] = u32x4{head_mask(k, 0), head_mask(k, 1), head_mask(k, 2), head_mask(k, 3)};
+        } else if (lane < 34) {
+            const uint32_t k = (uint32_t)lane - 17u;
+            L.nm[k] = u32x4{~head_mask(k, 0), ~head_mask(k, 1), ~head_mask(k, 2),
+                            ~head_mask(k, 3)};
+        }
+    }
     const uint32_t s = (uint32_t)(a & 15u);
     const uint32_t nch = valid ? (s + span + 15u) >> 4 : 0u;
     const uint32_t nsl = (nch + PK - 1u) / PK; // slots of PK chunks
@@ -310,7 +339,7 @@ __device__ __forceinline__ FlatTile flat_tile_setup(FlatLds<UN> &L, int lane, ui
 // groups.  Every issued group is summed: a load left pending at the loop's
 // exit makes hipcc wait vmcnt(0) at the loop head on every iteration
 // (measured in the ISA with a mid-loop exit).
-template <int UN, int KIND, bool NT, bool NOLOAD, bool ARITH, int PK>
+template <int UN, int KIND, bool NT, bool NOLOAD, bool ARITH, int PK, bool VSUM = false>
 __device__ __forceinline__ void flat_tile_loop(FlatRows<UN, PK> &A, FlatLds<UN> &L,
                                                const WeightLut *lut, int lane,
                                                const FlatTile &t, uint32_t &acc)
@@ -322,23 +351,23 @@ __device__ __forceinline__ void flat_tile_loop(FlatRows<UN, PK> &A, FlatLds<UN> 
         flat_issue<UN, NT, NOLOAD, PK, KIND>(B, L, j + kGrp, lane, t.cp, t.ce, t.rank,
                                              t.last_rank, t.total);
         __builtin_amdgcn_sched_barrier(0);
-        flat_accum<UN, KIND, ARITH, PK>(A, L, lut, j, lane, t.cp, t.ce, t.total, acc);
+        flat_accum<UN, KIND, ARITH, PK, VSUM>(A, L, lut, j, lane, t.cp, t.ce, t.total, acc);
         __builtin_amdgcn_sched_barrier(0);
         flat_issue<UN, NT, NOLOAD, PK, KIND>(A, L, j + 2 * kGrp, lane, t.cp, t.ce, t.rank,
                                              t.last_rank, t.total);
         __builtin_amdgcn_sched_barrier(0);
-        flat_accum<UN, KIND, ARITH, PK>(B, L, lut, j + kGrp, lane, t.cp, t.ce, t.total, acc);
+        flat_accum<UN, KIND, ARITH, PK, VSUM>(B, L, lut, j + kGrp, lane, t.cp, t.ce, t.total, acc);
         __builtin_amdgcn_sched_barrier(0);
     }
     if (j + kGrp < t.total) {
         flat_issue<UN, NT, NOLOAD, PK, KIND>(B, L, j + kGrp, lane, t.cp, t.ce, t.rank,
                                              t.last_rank, t.total);
         __builtin_amdgcn_sched_barrier(0);
-        flat_accum<UN, KIND, ARITH, PK>(A, L, lut, j, lane, t.cp, t.ce, t.total, acc);
+        flat_accum<UN, KIND, ARITH, PK, VSUM>(A, L, lut, j, lane, t.cp, t.ce, t.total, acc);
         __builtin_amdgcn_sched_barrier(0);
-        flat_accum<UN, KIND, ARITH, PK>(B, L, lut, j + kGrp, lane, t.cp, t.ce, t.total, acc);
+        flat_accum<UN, KIND, ARITH, PK, VSUM>(B, L, lut, j + kGrp, lane, t.cp, t.ce, t.total, acc);
     } else {
-        flat_accum<UN, KIND, ARITH, PK>(A, L, lut, j, lane, t.cp, t.ce, t.total, acc);
+        flat_accum<UN, KIND, ARITH, PK, VSUM>(A, L, lut, j, lane, t.cp, t.ce, t.total, acc);
     }
 }
 
@@ -346,7 +375,8 @@ __device__ __forceinline__ void flat_tile_loop(FlatRows<UN, PK> &A, FlatLds<UN> 
 // reference accumulator (in_cksum.c:140-167 / 107-120, mod 2^32) -- the
 // caller folds it.  `after_first_issue` runs once the tile's first row group
 // is in flight (the caller's next-tile prefetch goes there).
-template <int UN, int KIND, bool NT, bool NOLOAD, bool ARITH, class F, int PK = 1>
+template <int UN, int KIND, bool NT, bool NOLOAD, bool ARITH, class F, int PK = 1,
+          bool VSUM = false>
 __device__ __forceinline__ uint32_t flat_tile_sum(FlatLds<UN> &L, const WeightLut *lut,
                                                   int lane, uint64_t a, uint32_t len,
                                                   bool valid, const PseudoHdr &ph,
@@ -354,8 +384,8 @@ __device__ __forceinline__ uint32_t flat_tile_sum(FlatLds<UN> &L, const WeightLu
 {
     static_assert(PK == 1 || !NOLOAD, "diagnostic build: one chunk per slot");
     const uint32_t span = KIND == WC_KIND_PAYLOAD ? max(len, 20u) : len;
-    const FlatTile t = flat_tile_setup<UN, PK>(L, lane, a, len, span, valid,
-                                               len | (ph.hl << 16) | (ph.v4 << 24));
+    const FlatTile t = flat_tile_setup<UN, PK, VSUM>(L, lane, a, len, span, valid,
+                                                     len | (ph.hl << 16) | (ph.v4 << 24));
     uint32_t acc = ph.special;
     FlatRows<UN, PK> A;
     if (t.total != 0)
@@ -363,7 +393,12 @@ __device__ __forceinline__ uint32_t flat_tile_sum(FlatLds<UN> &L, const WeightLu
                                              t.total);
     after_first_issue();
     if (t.total != 0)
-        flat_tile_loop<UN, KIND, NT, NOLOAD, ARITH, PK>(A, L, lut, lane, t, acc);
+        flat_tile_loop<UN, KIND, NT, NOLOAD, ARITH, PK, VSUM>(A, L, lut, lane, t, acc);
+    if constexpr (VSUM) {
+        static_assert(KIND == WC_KIND_IP, "VSUM: plain ip_cksum");
+        if (a & 1u) // residue of the odd-start accumulator (fold-exact)
+            acc = __builtin_amdgcn_alignbit(acc, acc, 24);
+    }
     return acc;
 }
 

@@ -51,20 +51,6 @@ namespace {
 // packet cost 14 % of the C4 time (one more cache line per lane, not latency:
 // profiles/ab_r01_c4_payload_hdr.log).
 
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ uint32_t wsum(uint32_t x, uint32_t acc)
-{
-    return __builtin_amdgcn_udot2(__builtin_bit_cast(u16x2, x), u16x2{1, 1}, acc, false);
-}
-
-// 0xFF in the bytes of dword j that are among the first q bytes of a chunk.
-__device__ __forceinline__ uint32_t head_mask(uint32_t q, int j)
-{
-    const uint32_t nb = min(q - min(q, 4u * j), 4u);
-    return nb >= 4u ? 0xFFFFFFFFu : ((1u << (8u * nb)) - 1u);
-}
-
 // V of a chunk's first q bytes (q = 16: all of them).
 template <bool MASK>
 __device__ __forceinline__ uint32_t seg_chunk(const u32x4 &d, uint32_t q)
@@ -661,12 +647,14 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
                     ph = hdr_pseudo(hdr, a);
             }
             wave_order();
+            auto noop = [] {};
             if constexpr (KIND == WC_KIND_PAYLOAD)
                 r = fold_not(flat_tile_sum_payload<UN, NT, true>(L.flat, nullptr, lane, a, len,
-                                                                 valid, ph, hdr, [] {}));
-            else
-                r = fold_not(flat_tile_sum<UN, KIND, NT, false, true>(L.flat, nullptr, lane, a,
-                                                                      len, valid, ph, [] {}));
+                                                                 valid, ph, hdr, noop));
+            else // ip_cksum: word sums (VSUM), +0.5 point on the mixed-size ring
+                r = fold_not(flat_tile_sum<UN, KIND, NT, false, true, decltype(noop) &, 1,
+                                           KIND == WC_KIND_IP>(L.flat, nullptr, lane, a, len,
+                                                               valid, ph, noop));
             if constexpr (HDR)
                 rh = valid && ph.v4 ? lane_hdr_cksum<NT>(a, ph.hl, nullptr) : (uint16_t)0;
         }
