@@ -47,12 +47,14 @@ RAGGED_MODES = {
     "flat2": {"WC_SEG": "0", "WC_FLAT_PK": "2"},
     "seg": {"WC_SEG": "1", "WC_GRP_DENSE": "65", "WC_GRP_SPARSE": "65"},
     "grp": {"WC_SEG": "1", "WC_GRP_DENSE": "0", "WC_GRP_SPARSE": "0"},
+    "segflat": {"WC_SEG": "1", "WC_GATHER": "0"},
+    "gath": {"WC_SEG": "1", "WC_GATHER": "2", "WC_GRP_DENSE": "65", "WC_GRP_SPARSE": "65"},
     "default": {},
 }
 
 
 def ragged_mode(monkeypatch, mode: str) -> None:
-    for k in ("WC_SEG", "WC_GRP_DENSE", "WC_GRP_SPARSE", "WC_FLAT_PK", "WC_VARIANT"):
+    for k in ("WC_SEG", "WC_GRP_DENSE", "WC_GRP_SPARSE", "WC_FLAT_PK", "WC_VARIANT", "WC_GATHER"):
         monkeypatch.delenv(k, raising=False)
     for k, v in RAGGED_MODES[mode].items():
         monkeypatch.setenv(k, v)

@@ -19,6 +19,7 @@ for c in ${CASES:-c2:ip c2:payload}; do
     case $cfg in
         c2) a="--config c2" ;;
         c4) a="--config c4" ;;
+        c4r) a="--config c4r" ;;
         zslots) a="--config zslots" ;;
         slot) a="--config c3 --len 1500 --stride 2048 --offset 14" ;;
         rslot) a="--config c3 --len 1500 --stride 2048 --offset 14 --ragged" ;;

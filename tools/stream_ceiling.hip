@@ -49,3 +49,50 @@ extern "C" int stream_read(const void *buf, uint64_t bytes, int grid, int unroll
 #undef L
     return (int)hipGetLastError();
 }
+
+// Slot-read ceiling (measurement only): the lines a netmap ring of mixed
+// sizes touches -- packet i at base + i * stride + off, lens[i] bytes -- read
+// with G lanes per packet and the cheapest addressing (no checksum, no owner
+// lookup): each lane loads chunks k, k + G, ... of its packet's aligned chunk
+// range, two loads in flight per step.
+template <int G, bool NT>
+__global__ void __launch_bounds__(256) k_slot_read(const uint8_t *__restrict__ base,
+                                                   uint64_t stride, uint32_t off,
+                                                   const uint16_t *__restrict__ lens,
+                                                   uint64_t n, uint32_t *out)
+{
+    const uint64_t gid = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / G;
+    const uint64_t ngr = (uint64_t)gridDim.x * blockDim.x / G;
+    const uint32_t k = threadIdx.x % G;
+    uint32_t acc = 0;
+    for (uint64_t p = gid; p < n; p += ngr) {
+        const uint64_t a = (uint64_t)base + p * stride + off;
+        const uint64_t c0 = a & ~15ull;
+        const uint32_t nch = (uint32_t)((a & 15u) + lens[p] + 15u) >> 4;
+        for (uint32_t c = k; c < nch; c += 2 * G) {
+            const uint32_t c2 = min(c + G, nch - 1u);
+            gptr q0 = (gptr)(uintptr_t)(c0 + 16ull * c), q1 = (gptr)(uintptr_t)(c0 + 16ull * c2);
+            u32x4 v0 = NT ? __builtin_nontemporal_load(q0) : *q0;
+            u32x4 v1 = NT ? __builtin_nontemporal_load(q1) : *q1;
+            acc ^= v0.x ^ v0.y ^ v1.z ^ v1.w;
+        }
+    }
+    if (acc == 0x12345678u)
+        out[threadIdx.x] = acc;
+}
+
+extern "C" int slot_read(const void *base, uint64_t stride, uint32_t off, const void *lens,
+                         uint64_t n, int group, int grid, int nt, void *out, void *stream)
+{
+    hipStream_t st = (hipStream_t)stream;
+#define S(GG, N)                                                               \
+    hipLaunchKernelGGL((k_slot_read<GG, N>), dim3(grid), dim3(256), 0, st,     \
+                       (const uint8_t *)base, stride, off, (const uint16_t *)lens, n, \
+                       (uint32_t *)out)
+    if (group == 4) { if (nt) S(4, true); else S(4, false); }
+    else if (group == 8) { if (nt) S(8, true); else S(8, false); }
+    else if (group == 16) { if (nt) S(16, true); else S(16, false); }
+    else { if (nt) S(32, true); else S(32, false); }
+#undef S
+    return (int)hipGetLastError();
+}

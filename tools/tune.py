@@ -40,6 +40,9 @@ def stream_lib():
     lib = ctypes.CDLL(str(so))
     lib.stream_read.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
                                 ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    lib.slot_read.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p,
+                              ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                              ctypes.c_void_p, ctypes.c_void_p]
     return lib
 
 
@@ -82,15 +85,18 @@ def main():
     dev = torch.device("cuda:0")
     wc.gpu_init(0)
     stream = torch.cuda.current_stream()
-    if args.config in ("c4", "zslots"):
+    if args.config in ("c4", "c4r", "zslots"):
         # c4: Zipf lengths packed; zslots: the same lengths in 2048-B slots at
         # +14 (a netmap RX ring of mixed sizes)
-        n = args.packets if args.packets != (1 << 20) else (1 << 24 if args.config == "c4"
-                                                             else 1 << 21)
+        n = args.packets if args.packets != (1 << 20) else (1 << 21 if args.config == "zslots"
+                                                             else 1 << 24)
         lens = synth.zipf_lengths(n)
-        if args.config == "c4":
+        if args.config in ("c4", "c4r"):
             offs = synth.packed_offsets(lens)
             span = int(lens.astype(np.uint64).sum())
+            if args.config == "c4r":  # the same packets listed in random order
+                perm = np.random.default_rng(5).permutation(n)
+                offs, lens = offs[perm].copy(), lens[perm].copy()
         else:
             offs = (np.arange(n, dtype=np.uint64) * 2048 + 14).astype(np.uint64)
             span = n * 2048
@@ -132,7 +138,7 @@ def main():
     knobs = {"WC_SHAPE", "WC_NT", "WC_BLOCKS_PER_CU", "WC_GRID", "WC_FLAT_UN", "WC_FLAT_TPW",
              "WC_DIAG_NOLOAD", "WC_FLAT_MIN", "WC_RAGGED_SHAPE", "WC_VARIANT", "WC_SEG",
              "WC_SEG_ROWS", "WC_GRP_DENSE", "WC_GRP_SPARSE", "WC_GRP_ROWS",
-             "WC_STRIDED_SEG", "WC_FLAT_PK"}
+             "WC_STRIDED_SEG", "WC_FLAT_PK", "WC_GATHER"}
     knobs |= {kv.split("=", 1)[0] for v in variants for kv in v.split()}
     knobs |= {k for k in os.environ if k.startswith("WC_") and k != "WC_NO_BUILD"}
     base_env = {k: os.environ.get(k) for k in knobs}
@@ -153,10 +159,18 @@ def main():
     if args.ceiling:
         slib = stream_lib()
         sink = torch.zeros(1 << 22, dtype=torch.int32, device=dev)
-        for grid in (1024, 2048, 4096, 8192):
-            for unroll in (2, 4, 8):
-                for nt in (0, 1):
-                    cases.append((f"READ grid={grid} unroll={unroll} nt={nt}", (grid, unroll, nt)))
+        if args.config == "zslots":
+            # the ring's own lines, cheapest addressing (stream_ceiling.hip k_slot_read)
+            for grp in (4, 8, 16, 32):
+                for grid in (4096, 16384):
+                    for nt in (0, 1):
+                        cases.append((f"SLOTREAD G={grp} grid={grid} nt={nt}", (grp, grid, nt)))
+        else:
+            for grid in (1024, 2048, 4096, 8192):
+                for unroll in (2, 4, 8):
+                    for nt in (0, 1):
+                        cases.append((f"READ grid={grid} unroll={unroll} nt={nt}",
+                                      (grid, unroll, nt)))
 
     times = {c[0]: [] for c in cases}
     ref = None
@@ -186,6 +200,10 @@ def main():
                 g, u, nt = cfg
                 fn = lambda: slib.stream_read(buf.data_ptr(), nbytes, g, u, nt,  # noqa: E731
                                               sink.data_ptr(), stream.cuda_stream)
+                if name.startswith("SLOTREAD"):
+                    fn = lambda: slib.slot_read(buf.data_ptr(), 2048, 14,  # noqa: E731
+                                                d_len.data_ptr(), n, g, u, nt, sink.data_ptr(),
+                                                stream.cuda_stream)
                 fn()
                 ms = time_it(fn, args.iters, stream)
             times[name].append(ms)

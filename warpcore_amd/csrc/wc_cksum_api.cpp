@@ -110,6 +110,7 @@ struct Config {
     int grp_sparse = 40;           // WC_GRP_SPARSE
     int grp_rows = 4;              // WC_GRP_ROWS
     int flat_pk = 1;               // WC_FLAT_PK: flat kernel chunks per lane slot
+    int gather = 1;                // WC_GATHER: seg kernel's gathered-stream path (0 off, 2 forced)
 };
 
 std::mutex g_mu;
@@ -174,6 +175,7 @@ void load_config_locked()
     c.grp_sparse = env_int("WC_GRP_SPARSE", c.grp_sparse);
     c.grp_rows = env_int("WC_GRP_ROWS", c.grp_rows);
     c.flat_pk = env_int("WC_FLAT_PK", c.flat_pk);
+    c.gather = env_int("WC_GATHER", c.gather);
     g_cfg = c;
     g_cfg_loaded = true;
 }
@@ -417,6 +419,7 @@ int run(const Device &D, const Config &C, const wc::LaunchArgs &args, const Plan
     a.grp_thr = C.grp_dense | (C.grp_sparse << 8);
     a.grp_rows = C.grp_rows;
     a.flat_pk = C.flat_pk;
+    a.gather = C.gather;
     hipError_t e = p.shape.group == 0 ? wc::launch_flat(a, p.shape.unroll, st)
                                       : wc::launch_cksum(a, p.shape, p.grid, st);
     return hip_err(e);

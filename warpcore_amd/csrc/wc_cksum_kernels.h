@@ -103,6 +103,8 @@ struct LaunchArgs {
     int grp_thr = 65 | (40 << 8);
     int grp_rows = 4; // k_cksum_seg grouped path: rows per ping-pong group (2, 4)
     int flat_pk = 1;  // flat kernel: 16-byte chunks per lane slot (1, or 2 = 32 B per lane)
+    int gather = 1; // k_cksum_seg: gathered-stream path for tiles neither dense nor uniform
+                    // (0 = flat path, 2 = for dense tiles too: tests)
 };
 
 struct Shape {

@@ -99,18 +99,21 @@ __device__ __forceinline__ void seg_issue(SegRows<UNS> &R, uint64_t A0, uint32_t
 // also picks up its packet's first HC chunks c0, c0 + 1 (, c0 + 2) -- its
 // header bytes 0..11 (0..19 with the fused header checksum), and the start
 // chunk cs, which is c0 or c0 + 1.
-template <int UNS, int HC>
+template <int UNS, int HC, bool CLAMP>
 __device__ __forceinline__ void seg_accum(const SegRows<UNS> &R, uint32_t *pre, u32x4 *stage,
-                                          uint32_t g0, int lane, uint32_t cs, uint32_t ce,
-                                          uint32_t c0, uint32_t &carry, uint32_t &Ps,
-                                          uint32_t &Pe, u32x4 &hs, u32x4 &he, u32x4 &h1,
-                                          u32x4 &h2)
+                                          uint32_t g0, int lane, uint32_t T, uint32_t cs,
+                                          uint32_t ce, uint32_t c0, uint32_t &carry,
+                                          uint32_t &Ps, uint32_t &Pe, u32x4 &hs, u32x4 &he,
+                                          u32x4 &h1, u32x4 &h2)
 {
     constexpr uint32_t kGrp = 64u * UNS;
     uint32_t P[UNS];
 #pragma unroll
-    for (int u = 0; u < UNS; ++u)
+    for (int u = 0; u < UNS; ++u) {
         P[u] = seg_chunk<false>(R.d[u], 16u);
+        if constexpr (CLAMP) // a gathered stream's slots past T re-read its last chunk
+            P[u] = g0 + 64u * u + (uint32_t)lane < T ? P[u] : 0u;
+    }
 #define WC_SEG_STEP(CTRL, ROWS)                                                \
     _Pragma("unroll") for (int u = 0; u < UNS; ++u) P[u] += dpp0<CTRL, ROWS>(P[u]);
     WC_SEG_STEP(kDppRowShr + 1, 0xF)
@@ -193,26 +196,64 @@ __device__ __forceinline__ bool seg_payload_ok(uint64_t a, uint32_t len, const P
     return len >= max(ph.hl, 20u) && !seg_wrap_risk(a, len, ph);
 }
 
-// One dense tile.  [a, a + len) is this lane's packet; ip_cksum sums all of
-// it, payload_cksum the range [a + 8, a + len) corrected as below.  Returns
-// the checksum, or done = false when a payload_cksum lane can't be summed
-// here (header longer than the packet, possible uint32 wrap): the caller
-// then takes the exact flat path for the tile.
-template <int UNS, int KIND, bool NT, bool HDR>
+// Chunk sources of seg_tile: slot q of the tile's stream is
+//   * DenseSrc: the byte range itself, chunk A0 + 16 q (zero past T);
+//   * GathSrc: the tile's packets' own chunks in packet order (the flat
+//     path's slot numbering, its owner lookup for the address; slots past T
+//     re-read the last chunk and are zeroed in seg_accum).
+template <int UNS, bool NT>
+struct DenseSrc {
+    static constexpr bool kClamp = false;
+    uint64_t A0;
+    uint32_t T;
+    uint64_t zero;
+    __device__ __forceinline__ void issue(SegRows<UNS> &R, uint32_t g0, int lane) const
+    {
+        seg_issue<UNS, NT>(R, A0, g0, lane, T, zero);
+    }
+};
+
+template <int UNS, bool NT>
+struct GathSrc {
+    static constexpr bool kClamp = true;
+    FlatLds<UNS> *L;
+    FlatTile t;
+    __device__ __forceinline__ void issue(SegRows<UNS> &R, uint32_t g0, int lane) const
+    {
+        FlatRows<UNS, 1> F;
+        flat_issue<UNS, NT>(F, *L, g0, lane, t.cp, t.ce, t.rank, t.last_rank, t.total);
+#pragma unroll
+        for (int u = 0; u < UNS; ++u)
+            R.d[u] = F.d[u][0];
+    }
+};
+
+// One tile as a stream of T chunk slots.  [a, a + len) is this lane's packet,
+// starting ra bytes into the stream (dense: a - A0; gathered: 16 cp + (a &
+// 15), so a packet's bytes keep their address parity and position within a
+// chunk); ip_cksum sums all of it, payload_cksum the range [a + 8, a + len)
+// corrected as below.  Returns the checksum, or done = false when a
+// payload_cksum lane can't be summed here (header longer than the packet,
+// possible uint32 wrap): the caller then takes the exact flat path for the
+// tile.  On a gathered stream a packet's first and last chunks hold other
+// bytes of the same cache lines; they cancel like the gaps of a dense range.
+template <int UNS, int KIND, bool NT, bool HDR, class Src>
 __device__ __forceinline__ uint16_t seg_tile(uint32_t *pre, u32x4 *stage, int lane, uint64_t a,
-                                             uint32_t len, bool valid, uint64_t A0, uint32_t T,
-                                             uint64_t zero, bool &done, uint16_t &rh)
+                                             uint64_t ra, uint32_t len, bool valid, uint32_t T,
+                                             const Src &src, uint64_t zero, bool &done,
+                                             uint16_t &rh)
 {
     constexpr uint32_t kGrp = 64u * UNS;
     constexpr bool PL = KIND == WC_KIND_PAYLOAD;
     constexpr int HC = PL ? (HDR ? 3 : 2) : 0;
-    const uint64_t rs = a + (PL ? 8u : 0u) - A0, re = a + len - A0;
+    constexpr bool CL = Src::kClamp;
+    const uint64_t rs = ra + (PL ? 8u : 0u), re = ra + len;
     const uint32_t cs = (uint32_t)(rs >> 4), qs = (uint32_t)(rs & 15u);
     const uint32_t ce = (uint32_t)(re >> 4), qe = (uint32_t)(re & 15u);
-    const uint32_t c0 = (uint32_t)((a - A0) >> 4);
+    const uint32_t c0 = (uint32_t)(ra >> 4);
 
     SegRows<UNS> A, B;
-    seg_issue<UNS, NT>(A, A0, 0, lane, T, zero);
+    src.issue(A, 0, lane);
 
     uint32_t carry = 0, Ps = 0, Pe = 0;
     u32x4 hs = {0u, 0u, 0u, 0u}, he = {0u, 0u, 0u, 0u}, h1 = {0u, 0u, 0u, 0u},
@@ -223,29 +264,32 @@ __device__ __forceinline__ uint16_t seg_tile(uint32_t *pre, u32x4 *stage, int la
     // the rows summed round up to one group, not two (a 17-row tile sums
     // 20 rows instead of 24).
     uint32_t j = 0;
+#define WC_SEG_ACC(R, G)                                                       \
+    seg_accum<UNS, HC, CL>(R, pre, stage, G, lane, T, cs, ce, c0, carry, Ps, Pe, hs, he, h1, h2)
     for (; j + 2 * kGrp < T; j += 2 * kGrp) {
-        seg_issue<UNS, NT>(B, A0, j + kGrp, lane, T, zero);
+        src.issue(B, j + kGrp, lane);
         __builtin_amdgcn_sched_barrier(0);
-        seg_accum<UNS, HC>(A, pre, stage, j, lane, cs, ce, c0, carry, Ps, Pe, hs, he, h1, h2);
+        WC_SEG_ACC(A, j);
         __builtin_amdgcn_sched_barrier(0);
-        seg_issue<UNS, NT>(A, A0, j + 2 * kGrp, lane, T, zero);
+        src.issue(A, j + 2 * kGrp, lane);
         __builtin_amdgcn_sched_barrier(0);
-        seg_accum<UNS, HC>(B, pre, stage, j + kGrp, lane, cs, ce, c0, carry, Ps, Pe, hs, he, h1,
-                           h2);
+        WC_SEG_ACC(B, j + kGrp);
         __builtin_amdgcn_sched_barrier(0);
     }
     if (j + kGrp < T) {
-        seg_issue<UNS, NT>(B, A0, j + kGrp, lane, T, zero);
+        src.issue(B, j + kGrp, lane);
         __builtin_amdgcn_sched_barrier(0);
-        seg_accum<UNS, HC>(A, pre, stage, j, lane, cs, ce, c0, carry, Ps, Pe, hs, he, h1, h2);
+        WC_SEG_ACC(A, j);
         __builtin_amdgcn_sched_barrier(0);
-        seg_accum<UNS, HC>(B, pre, stage, j + kGrp, lane, cs, ce, c0, carry, Ps, Pe, hs, he, h1,
-                           h2);
+        WC_SEG_ACC(B, j + kGrp);
         j += 2 * kGrp;
     } else {
-        seg_accum<UNS, HC>(A, pre, stage, j, lane, cs, ce, c0, carry, Ps, Pe, hs, he, h1, h2);
+        WC_SEG_ACC(A, j);
         j += kGrp;
     }
+#undef WC_SEG_ACC
+    if (cs >= j) // an empty packet at the stream's end (gathered streams)
+        Ps = carry;
     if (ce >= j) // the packet ends exactly at the last row group's end
         Pe = carry;
     done = true;
@@ -554,7 +598,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UNS >=
 k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
             const uint16_t *__restrict__ lens, uint64_t n, uint16_t *__restrict__ out,
             unsigned long long *__restrict__ bad, int grp_thr, int variant, uint64_t stride,
-            uint32_t slen, uint16_t *__restrict__ out_hdr)
+            uint32_t slen, uint16_t *__restrict__ out_hdr, int gather)
 {
     static_assert(!HDR || KIND == WC_KIND_PAYLOAD, "header checksum rides on payload");
     union TileLds {
@@ -564,6 +608,10 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
             u32x4 stage[64 * UNS]; // the row group's chunks
             uint32_t pre[64 * UNS];
         } seg;
+        struct {
+            FlatLds<UNS> f; // slot table, row marks, prefix sums
+            u32x4 stage[64 * UNS];
+        } gat;
     };
     __shared__ TileLds lds_all[kFlatWaves];
 
@@ -618,6 +666,8 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
         } else {
             dense = seg_dense(lane, a, len, valid, nvalid, A0, T);
         }
+        if (gather == 2) // WC_GATHER=2 (tests): every non-uniform tile on the gathered path
+            dense = false;
         // Uniform tile?  Chunk fill of the grouped path's 1024 R slots --
         // only computed when the threshold for this kind of tile can be met
         // (dense tiles never take the grouped path by default).
@@ -636,8 +686,19 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
         if (grouped)
             r = grp_tile<UNG, KIND, NT, HDR>(L.grp, lane, a, len, valid, Rq, zero, done, rh);
         else if (dense)
-            r = seg_tile<UNS, KIND, NT, HDR>(L.seg.pre, L.seg.stage, lane, a, len, valid, A0, T,
-                                             zero, done, rh);
+            r = seg_tile<UNS, KIND, NT, HDR>(L.seg.pre, L.seg.stage, lane, a, a - A0, len, valid,
+                                             T, DenseSrc<UNS, NT>{A0, T, zero}, zero, done, rh);
+        else if (!HDR && gather) { // (the fused header variant keeps the flat path: no spills)
+            // Gathered stream: the tile's packets' chunks in packet order
+            // (sparse or unordered tiles -- a netmap ring of mixed sizes).
+            const uint32_t span = KIND == WC_KIND_PAYLOAD ? max(len, 20u) : len;
+            const FlatTile t = flat_tile_setup<UNS, 1>(L.gat.f, lane, a, len, span, valid, 0u);
+            if (t.total != 0)
+                r = seg_tile<UNS, KIND, NT, HDR>(L.gat.f.pre, L.gat.stage, lane, a,
+                                                 16ull * t.cp + (a & 15u), len, valid, t.total,
+                                                 GathSrc<UNS, NT>{&L.gat.f, t}, zero, done, rh);
+            wave_order(); // the flat path below rewrites the tables
+        }
         if (!done) {
             PseudoHdr ph{0u, 1u, 0u};
             HdrRaw hdr{};
@@ -689,13 +750,13 @@ static hipError_t launch_seg_kernel(const LaunchArgs &a, hipStream_t st)
             return hipErrorInvalidValue;
         hipLaunchKernelGGL((k_cksum_seg<UN, 4, 4, WC_KIND_PAYLOAD, true, false, true>),
                            dim3(grid), dim3(256), 0, st, b, a.offs, a.lens, a.n, a.out, bad,
-                           a.grp_thr, a.variant, a.stride, a.len, a.out_hdr);
+                           a.grp_thr, a.variant, a.stride, a.len, a.out_hdr, (int)a.gather);
         return hipGetLastError();
     }
 #define WC_SEG_K(K, S)                                                         \
     hipLaunchKernelGGL((k_cksum_seg<UN, US, UG, K, true, S>), dim3(grid), dim3(256), 0, st, \
                        b, a.offs, a.lens, a.n, a.out, bad, a.grp_thr, a.variant, a.stride, \
-                       a.len, nullptr)
+                       a.len, nullptr, (int)a.gather)
 #define WC_SEG(US_, UG_)                                                       \
     {                                                                          \
         constexpr int US = US_, UG = UG_;                                      \
