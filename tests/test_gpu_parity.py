@@ -152,6 +152,18 @@ def test_planner_shapes(gpu, monkeypatch, base, stride, length, kind, shape):
     assert (p["group"], p["chunks_per_lane"], p["unroll"]) == shape
 
 
+@pytest.mark.parametrize("length,seg", [(64, False), (80, True), (144, True), (240, True),
+                                        (256, False), (288, False)])
+def test_planner_aligned_small_take_seg(gpu, monkeypatch, length, seg):
+    """Packed aligned 5..16-chunk packets (stride % 64 != 0) take the seg
+    kernel (group 0 in the plan), 64 / 256 B and longer ones the group kernel."""
+    for k in ("WC_SHAPE", "WC_STRIDED_SEG", "WC_VARIANT"):
+        monkeypatch.delenv(k, raising=False)
+    wc.reload_config()
+    p = wc.plan_strided(0x100000000, length, length, 1 << 20, kind="ip")
+    assert (p["group"] == 0) == seg
+
+
 def test_capped_grid_overlapping_stride(gpu):
     """More packets than one grid can hold: 2^26 + 1000 overlapping 3000-B
     packets at stride 16 take the (64,4,1) shape (one packet per wave), whose
@@ -176,8 +188,9 @@ def test_capped_grid_overlapping_stride(gpu):
 
 
 @pytest.mark.parametrize("sseg", ["0", "1", "2"])
-@pytest.mark.parametrize("length", [1, 2, 15, 16, 17, 63, 64, 65, 100, 111, 128, 255, 256, 257,
-                                    400, 500, 512, 513, 576, 577, 767, 768, 1472, 1500, 9000])
+@pytest.mark.parametrize("length", [1, 2, 15, 16, 17, 63, 64, 65, 80, 96, 100, 111, 128, 144, 160,
+                                    240, 255, 256, 257, 400, 500, 512, 513, 576, 577, 767, 768,
+                                    1472, 1500, 9000])
 def test_strided_packed_seg(gpu, monkeypatch, length, sseg):
     """Packed strided batches (stride = len .. len + len / 8) through the seg
     kernel with computed offsets (WC_STRIDED_SEG: 0 = group kernel only,

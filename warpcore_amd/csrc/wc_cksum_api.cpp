@@ -363,14 +363,22 @@ Plan plan_strided(const Device &D, const Config &C, uint64_t base, uint64_t stri
     //   36..48 chunks      group kernel (550-700 B: 84-89 % vs seg 83-84 %)
     //   >= 90 chunks       group kernel
     //   otherwise          seg, 4-row groups (300 B: 84 % vs group 69 %)
+    // Aligned unmasked (FULL) packets of 5..16 chunks at a stride that is not
+    // a multiple of 64 take the seg kernel too: the group kernel leaves most
+    // of its lane slots dead there (80..240 B packed: 64-77 % vs seg 71-85 %;
+    // 64 / 128 / 256 B, whose packets share cache-line phases, keep the
+    // group kernel: profiles/sweep_r02_small_aligned.log), 2-row groups up to
+    // 9 chunks, 4-row groups above.
     // WC_STRIDED_SEG = 0 never, 2 always (no fused header), 1 = the table;
     // WC_SEG_ROWS forces the row-group size.
     const int sseg = C.strided_seg;
     const bool packed = len != 0 && stride >= len && stride <= len + len / 8u;
-    const bool seg_table = stride % 64 != 0 && nch > 5 && !(nch >= 36 && nch <= 48) && nch < 90;
-    if (!hdr && !p.full && n >= 64 && packed && (sseg == 2 || (sseg == 1 && seg_table))) {
+    const bool seg_table =
+        stride % 64 != 0 &&
+        (p.full ? nch >= 5 && nch <= 16 : nch > 5 && !(nch >= 36 && nch <= 48) && nch < 90);
+    if (!hdr && n >= 64 && packed && (sseg == 2 || (sseg == 1 && seg_table))) {
         p.shape = {0, 1, C.flat_un};
-        p.seg_rows = C.seg_rows_set ? C.seg_rows : (nch <= 14 ? 2 : 4);
+        p.seg_rows = C.seg_rows_set ? C.seg_rows : (nch <= (p.full ? 9u : 14u) ? 2 : 4);
         p.grid = 0;
     }
     return p;

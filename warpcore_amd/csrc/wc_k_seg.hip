@@ -666,7 +666,7 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
         } else {
             dense = seg_dense(lane, a, len, valid, nvalid, A0, T);
         }
-        if (gather == 2) // WC_GATHER=2 (tests): every non-uniform tile on the gathered path
+        if (!STR && gather == 2) // WC_GATHER=2 (tests): every non-uniform tile gathered
             dense = false;
         // Uniform tile?  Chunk fill of the grouped path's 1024 R slots --
         // only computed when the threshold for this kind of tile can be met
@@ -688,7 +688,7 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
         else if (dense)
             r = seg_tile<UNS, KIND, NT, HDR>(L.seg.pre, L.seg.stage, lane, a, a - A0, len, valid,
                                              T, DenseSrc<UNS, NT>{A0, T, zero}, zero, done, rh);
-        else if (!HDR && gather) { // (the fused header variant keeps the flat path: no spills)
+        else if (!STR && !HDR && gather) { // (the fused header variant keeps the flat path: no spills)
             // Gathered stream: the tile's packets' chunks in packet order
             // (sparse or unordered tiles -- a netmap ring of mixed sizes).
             const uint32_t span = KIND == WC_KIND_PAYLOAD ? max(len, 20u) : len;

@@ -47,8 +47,16 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
     const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
     uint32_t nbad = 0;
     const uint64_t zero = (uint64_t)(uintptr_t)&kZeroChunk;
+    // A wave-iteration's results are PPW consecutive uint16s: with PPW <= 64
+    // one store instruction of lane j = packet p0 + j writes them (one
+    // coalesced store instead of U partial ones from the group leaders).  The
+    // leaders' scattered 2-byte stores cost C3 64 B 2 of its 11.5 us.
+    // WC_VARIANT bit 128 keeps the leader stores (A/B).
+    constexpr bool kLaneStore = PPW <= 64;
+    const bool lane_store = kLaneStore && !(variant & 128);
 
     for (uint64_t p0 = wave * PPW; p0 < n; p0 += nwaves * PPW) {
+        uint32_t res = 0, res_h = 0;
         uint64_t c0[U];
         uint32_t nch[U], plen[U];
         int s[U];
@@ -144,14 +152,38 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
             uint32_t Sh = 0;
             if constexpr (HDR)
                 Sh = group_sum<G>(combine(Eh, Oh, s[u] & 1));
+            if (lane_store) {
+                // Lane j of the wave takes packet p0 + j's result from its
+                // group (every lane of a group holds the sum).
+                const int src = (lane % GPW) * G;
+                const uint32_t r = __shfl((uint32_t)fold_not(S), src, 64);
+                if (lane / GPW == u)
+                    res = r;
+                if constexpr (HDR) {
+                    const uint32_t rh = __shfl(ph.v4 ? (uint32_t)fold_not(Sh) : 0u, src, 64);
+                    if (lane / GPW == u)
+                        res_h = rh;
+                }
+                continue;
+            }
             if (gl == 0 && valid[u]) {
                 const uint64_t i = p0 + (uint64_t)u * GPW + grp;
                 const uint16_t r = fold_not(S);
-                if (out)
+                if (out && !(variant & 64)) // WC_VARIANT bit 64: no result store (timing only)
                     out[i] = r;
                 nbad += r != 0;
                 if constexpr (HDR)
                     out_hdr[i] = ph.v4 ? fold_not(Sh) : 0; // ip4.c:110-115
+            }
+        }
+        if (lane_store) {
+            const uint64_t i = p0 + (uint64_t)lane;
+            if (lane < (int)PPW && i < n) {
+                if (out && !(variant & 64)) // WC_VARIANT bit 64: no result store (timing only)
+                    out[i] = (uint16_t)res;
+                nbad += res != 0;
+                if constexpr (HDR)
+                    out_hdr[i] = (uint16_t)res_h; // ip4.c:110-115
             }
         }
     }
