@@ -164,6 +164,17 @@ def test_planner_aligned_small_take_seg(gpu, monkeypatch, length, seg):
     assert (p["group"] == 0) == seg
 
 
+@pytest.mark.parametrize("length,seg", [(64, True), (256, True), (576, True), (992, True),
+                                        (1024, False), (1472, False)])
+def test_planner_payload_packed_take_seg(gpu, monkeypatch, length, seg):
+    """payload_cksum: packed packets below 64 chunks take the seg kernel at any stride."""
+    for k in ("WC_SHAPE", "WC_STRIDED_SEG", "WC_VARIANT"):
+        monkeypatch.delenv(k, raising=False)
+    wc.reload_config()
+    p = wc.plan_strided(0x100000000, length, length, 1 << 20, kind="payload")
+    assert (p["group"] == 0) == seg
+
+
 def test_capped_grid_overlapping_stride(gpu):
     """More packets than one grid can hold: 2^26 + 1000 overlapping 3000-B
     packets at stride 16 take the (64,4,1) shape (one packet per wave), whose

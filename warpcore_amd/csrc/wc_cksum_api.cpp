@@ -369,16 +369,24 @@ Plan plan_strided(const Device &D, const Config &C, uint64_t base, uint64_t stri
     // 64 / 128 / 256 B, whose packets share cache-line phases, keep the
     // group kernel: profiles/sweep_r02_small_aligned.log), 2-row groups up to
     // 9 chunks, 4-row groups above.
+    // payload_cksum: packed packets below 64 chunks take the seg kernel at any
+    // stride -- it reads the header bytes from its own stream, where the group
+    // kernel exchanges them between lanes (64 B 46 -> 56 %, 192 B 54 -> 82 %,
+    // 576 B 74-77 -> 83-84 %, 900 B 78 -> 84 %; from 64 chunks on the group
+    // kernel's 87-92 % wins: profiles/sweep_r02_payload_seg.log).
     // WC_STRIDED_SEG = 0 never, 2 always (no fused header), 1 = the table;
     // WC_SEG_ROWS forces the row-group size.
     const int sseg = C.strided_seg;
+    const bool payload = kind == WC_CKSUM_PAYLOAD;
     const bool packed = len != 0 && stride >= len && stride <= len + len / 8u;
     const bool seg_table =
-        stride % 64 != 0 &&
-        (p.full ? nch >= 5 && nch <= 16 : nch > 5 && !(nch >= 36 && nch <= 48) && nch < 90);
+        payload ? nch < 64
+                : stride % 64 != 0 && (p.full ? nch >= 5 && nch <= 16
+                                              : nch > 5 && !(nch >= 36 && nch <= 48) && nch < 90);
     if (!hdr && n >= 64 && packed && (sseg == 2 || (sseg == 1 && seg_table))) {
         p.shape = {0, 1, C.flat_un};
-        p.seg_rows = C.seg_rows_set ? C.seg_rows : (nch <= (p.full ? 9u : 14u) ? 2 : 4);
+        const uint32_t rows2 = payload ? 5u : (p.full ? 9u : 14u);
+        p.seg_rows = C.seg_rows_set ? C.seg_rows : (nch <= rows2 ? 2 : 4);
         p.grid = 0;
     }
     return p;
