@@ -223,8 +223,10 @@ def make_workload(args, dev, rank, world):
                     f"(mean {nbytes / n:.1f}) in {slot}-B slots at +{at}, ragged batch")
             meta = {"packets_per_gpu": n, "mean_packet_bytes": round(nbytes / n, 2),
                     "slot_bytes": slot, "layout": "ragged", "kind": kind}
-        plan = {"kernel": "seg (grouped path for uniform tiles)",
-                "rows_per_group": int(os.environ.get("WC_GRP_ROWS", "4")),
+        path = "grouped path" if args.config == "slots" else "gathered-stream path"
+        plan = {"kernel": f"seg ({path} for these tiles)",
+                "rows_per_group": int(os.environ.get(
+                    "WC_GRP_ROWS" if args.config == "slots" else "WC_SEG_ROWS", "4")),
                 "grid": int((n + 255) // 256)}
         return step, n, nbytes, buf, out, plan, desc, meta, (offs, lens), "weak"
     # C4: Zipf(1) lengths 64..1472 B, packed with no padding (unaligned starts)

@@ -180,7 +180,7 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
             const uint64_t i = p0 + (uint64_t)lane;
             if (lane < (int)PPW && i < n) {
                 if (out && !(variant & 64)) // WC_VARIANT bit 64: no result store (timing only)
-                    out[i] = (uint16_t)res;
+                    out[i] = (uint16_t)res; // (a nontemporal store measured the same)
                 nbad += res != 0;
                 if constexpr (HDR)
                     out_hdr[i] = (uint16_t)res_h; // ip4.c:110-115
