@@ -594,7 +594,10 @@ __device__ __forceinline__ bool seg_dense(int lane, uint64_t a, uint32_t len, bo
 // which the seg path streams better than the group kernel masks its
 // boundary chunks; offsets and lengths are computed, not loaded.
 template <int UN, int UNS, int UNG, int KIND, bool NT, bool STR, bool HDR = false>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UNS >= 8 ? 2 : 4)))
+#ifndef WC_SEG_WAVES
+#define WC_SEG_WAVES 4 // waves per SIMD the 2/4-row variants are register-capped for
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UNS >= 8 ? 2 : WC_SEG_WAVES)))
 k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
             const uint16_t *__restrict__ lens, uint64_t n, uint16_t *__restrict__ out,
             unsigned long long *__restrict__ bad, int grp_thr, int variant, uint64_t stride,
