@@ -1,6 +1,6 @@
 // wc_k_seg.hip -- ragged (and packed strided) batches on gfx950: the
-// segmented-prefix tile kernel k_cksum_seg with its grouped and flat tile
-// paths, and the ragged launch entry point.
+// segmented-prefix tile kernel k_cksum_seg with its grouped, gathered and
+// flat tile paths, and the ragged launch entry point.
 #include "wc_flat.h"
 
 namespace wc {
