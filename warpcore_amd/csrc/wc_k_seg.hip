@@ -3,6 +3,8 @@
 // flat tile paths, and the ragged launch entry point.
 #include "wc_flat.h"
 
+#include <type_traits>
+
 namespace wc {
 namespace {
 
@@ -597,25 +599,38 @@ template <int UN, int UNS, int UNG, int KIND, bool NT, bool STR, bool HDR = fals
 #ifndef WC_SEG_WAVES
 #define WC_SEG_WAVES 4 // waves per SIMD the 2/4-row variants are register-capped for
 #endif
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(UNS >= 8 ? 2 : WC_SEG_WAVES)))
+#ifndef WC_SEG_STR_WAVES
+#define WC_SEG_STR_WAVES 4 // the same for packed strided ip_cksum (seg path only)
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
+    UNS >= 8 ? 2 : (STR && KIND == WC_KIND_IP ? WC_SEG_STR_WAVES : WC_SEG_WAVES))))
 k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
             const uint16_t *__restrict__ lens, uint64_t n, uint16_t *__restrict__ out,
             unsigned long long *__restrict__ bad, int grp_thr, int variant, uint64_t stride,
             uint32_t slen, uint16_t *__restrict__ out_hdr, int gather)
 {
     static_assert(!HDR || KIND == WC_KIND_PAYLOAD, "header checksum rides on payload");
-    union TileLds {
+    // Packed strided ip_cksum: every tile is dense and the seg path always
+    // completes, so the other paths (and their registers and LDS) are not
+    // compiled in.
+    constexpr bool kSegOnly = STR && KIND == WC_KIND_IP;
+    struct SegLds {
+        u32x4 stage[64 * UNS]; // the row group's chunks
+        uint32_t pre[64 * UNS];
+    };
+    union FullLds {
         FlatLds<UN> flat;
         GrpLds grp;
-        struct {
-            u32x4 stage[64 * UNS]; // the row group's chunks
-            uint32_t pre[64 * UNS];
-        } seg;
+        SegLds seg;
         struct {
             FlatLds<UNS> f; // slot table, row marks, prefix sums
             u32x4 stage[64 * UNS];
         } gat;
     };
+    struct SegOnlyLds {
+        SegLds seg;
+    };
+    using TileLds = typename std::conditional<kSegOnly, SegOnlyLds, FullLds>::type;
     __shared__ TileLds lds_all[kFlatWaves];
 
     const int lane = threadIdx.x & 63;
@@ -677,7 +692,7 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
         const uint32_t thr = dense ? (uint32_t)(grp_thr & 0xFF) : (uint32_t)(grp_thr >> 8);
         uint32_t Rq = 0;
         bool grouped = false;
-        if (thr <= 64u) {
+        if (!kSegOnly && thr <= 64u) {
             const uint32_t span = grp_span<KIND>(len);
             const uint32_t nchg = valid ? ((uint32_t)(a & 15u) + span + 15u) >> 4 : 0u;
             Rq = (wave_max(nchg) + 15u) >> 4;
@@ -686,7 +701,10 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
         }
         bool done = false;
         uint16_t rh = 0;
-        if (grouped)
+        if constexpr (kSegOnly)
+            r = seg_tile<UNS, KIND, NT, HDR>(L.seg.pre, L.seg.stage, lane, a, a - A0, len, valid,
+                                             T, DenseSrc<UNS, NT>{A0, T, zero}, zero, done, rh);
+        else if (grouped)
             r = grp_tile<UNG, KIND, NT, HDR>(L.grp, lane, a, len, valid, Rq, zero, done, rh);
         else if (dense)
             r = seg_tile<UNS, KIND, NT, HDR>(L.seg.pre, L.seg.stage, lane, a, a - A0, len, valid,
@@ -702,7 +720,7 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
                                                  GathSrc<UNS, NT>{&L.gat.f, t}, zero, done, rh);
             wave_order(); // the flat path below rewrites the tables
         }
-        if (!done) {
+        if constexpr (!kSegOnly) if (!done) {
             PseudoHdr ph{0u, 1u, 0u};
             HdrRaw hdr{};
             if constexpr (KIND == WC_KIND_PAYLOAD) {
