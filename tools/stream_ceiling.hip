@@ -96,3 +96,57 @@ extern "C" int slot_read(const void *base, uint64_t stride, uint32_t off, const 
 #undef S
     return (int)hipGetLastError();
 }
+
+// Tile-read probe (measurement only): does the checksum's ragged tile
+// structure -- each wave streaming its own contiguous region of R bytes in
+// 1-KiB rows, 4-row groups ping-ponged -- cost HBM rate by itself?
+//   mode 0: wave w reads region w (the seg kernel's layout: the resident
+//           waves' streams are R bytes apart);
+//   mode 1: the 4 waves of a block interleave their rows over the block's
+//           4 regions (the block streams one contiguous range).
+template <int GR>
+__global__ void __launch_bounds__(256) k_tile_read(const uint8_t *__restrict__ base,
+                                                   uint64_t region, uint64_t nregions, int mode,
+                                                   uint32_t *out)
+{
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t reg = (uint64_t)blockIdx.x * 4 + w;
+    if (reg >= nregions)
+        return;
+    const uint64_t rows = region / 1024;
+    uint32_t acc = 0;
+    for (uint64_t r = 0; r < rows; r += GR) {
+        u32x4 v[GR];
+#pragma unroll
+        for (int u = 0; u < GR; ++u) {
+            const uint64_t row = r + u;
+            uint64_t off;
+            if (mode == 0)
+                off = reg * region + row * 1024;
+            else // block-interleaved: global row index within the block's 4 regions
+                off = (uint64_t)blockIdx.x * 4 * region + (row * 4 + w) * 1024;
+            gptr q = (gptr)(uintptr_t)(base + off + 16 * lane);
+            v[u] = __builtin_nontemporal_load(q);
+        }
+#pragma unroll
+        for (int u = 0; u < GR; ++u)
+            acc ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
+    }
+    if (acc == 0x12345678u)
+        out[threadIdx.x] = acc;
+}
+
+extern "C" int tile_read(const void *base, uint64_t bytes, uint64_t region, int mode, int rows,
+                         void *out, void *stream)
+{
+    const uint64_t nreg = bytes / region;
+    const int grid = (int)((nreg + 3) / 4);
+    hipStream_t st = (hipStream_t)stream;
+    if (rows == 8)
+        hipLaunchKernelGGL((k_tile_read<8>), dim3(grid), dim3(256), 0, st, (const uint8_t *)base,
+                           region, nreg, mode, (uint32_t *)out);
+    else
+        hipLaunchKernelGGL((k_tile_read<4>), dim3(grid), dim3(256), 0, st, (const uint8_t *)base,
+                           region, nreg, mode, (uint32_t *)out);
+    return (int)hipGetLastError();
+}

@@ -40,6 +40,8 @@ def stream_lib():
     lib = ctypes.CDLL(str(so))
     lib.stream_read.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
                                 ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    lib.tile_read.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int,
+                              ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
     lib.slot_read.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p,
                               ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                               ctypes.c_void_p, ctypes.c_void_p]
@@ -166,6 +168,11 @@ def main():
                     for nt in (0, 1):
                         cases.append((f"SLOTREAD G={grp} grid={grid} nt={nt}", (grp, grid, nt)))
         else:
+            for region in (4096, 8192, 16384, 32768, 65536):
+                for mode in (0, 1):
+                    for rows in (4,):
+                        cases.append((f"TILEREAD region={region} mode={mode} rows={rows}",
+                                      (region, mode, rows)))
             for grid in (1024, 2048, 4096, 8192):
                 for unroll in (2, 4, 8):
                     for nt in (0, 1):
@@ -200,6 +207,9 @@ def main():
                 g, u, nt = cfg
                 fn = lambda: slib.stream_read(buf.data_ptr(), nbytes, g, u, nt,  # noqa: E731
                                               sink.data_ptr(), stream.cuda_stream)
+                if name.startswith("TILEREAD"):
+                    fn = lambda: slib.tile_read(buf.data_ptr(), nbytes, g, u, nt,  # noqa: E731
+                                                sink.data_ptr(), stream.cuda_stream)
                 if name.startswith("SLOTREAD"):
                     fn = lambda: slib.slot_read(buf.data_ptr(), 2048, 14,  # noqa: E731
                                                 d_len.data_ptr(), n, g, u, nt, sink.data_ptr(),
