@@ -387,6 +387,28 @@ __device__ __forceinline__ uint32_t group_sum(uint32_t v)
     return v;
 }
 
+constexpr int kDppRowBcast15Ctl = 0x142; // row_bcast:15 (DPP controls below)
+
+// Lane N of each aligned group of G >= 16 lanes, in every lane of the group:
+// DPP row_newbcast (one 16-lane row), plus row_bcast:15 into the odd rows
+// for G = 32 (lane 15 of rows 0 / 2 then holds their lane N), readlane for
+// G = 64.
+template <int G, int N>
+__device__ __forceinline__ uint32_t group_bcast(uint32_t v)
+{
+    static_assert(G == 16 || G == 32 || G == 64, "row-based groups");
+    if constexpr (G == 64) {
+        return (uint32_t)__builtin_amdgcn_readlane((int)v, N);
+    } else {
+        const uint32_t t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x150 + N, 0xF, 0xF,
+                                                                 false);
+        if constexpr (G == 16)
+            return t;
+        return (uint32_t)__builtin_amdgcn_update_dpp((int)t, (int)t, kDppRowBcast15Ctl, 0xA, 0xF,
+                                                     false);
+    }
+}
+
 constexpr int kFlatWaves = 4; // 256-thread blocks
 
 // DPP controls (GFX9 family, gfx950 included).

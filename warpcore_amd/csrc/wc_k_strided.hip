@@ -114,13 +114,43 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
                 // Header bytes 0, 2, 3, 6 sit in the group's chunks 0/1, i.e.
                 // in d[u][0] of group lanes 0 and 1.
                 const int su = s[u];
-                const uint32_t b0 = __shfl(pick_byte(d[u][0], su), lead + (su >> 4), 64);
-                const uint32_t b2 = __shfl(pick_byte(d[u][0], (su + 2) & 15),
-                                           lead + ((su + 2) >> 4), 64);
-                const uint32_t b3 = __shfl(pick_byte(d[u][0], (su + 3) & 15),
-                                           lead + ((su + 3) >> 4), 64);
-                const uint32_t b6 = __shfl(pick_byte(d[u][0], (su + 6) & 15),
-                                           lead + ((su + 6) >> 4), 64);
+                uint32_t b0, b2, b3, b6;
+                auto exchange = [&] { // ds_bpermute from the lane holding each byte
+                    b0 = __shfl(pick_byte(d[u][0], su), lead + (su >> 4), 64);
+                    b2 = __shfl(pick_byte(d[u][0], (su + 2) & 15), lead + ((su + 2) >> 4), 64);
+                    b3 = __shfl(pick_byte(d[u][0], (su + 3) & 15), lead + ((su + 3) >> 4), 64);
+                    b6 = __shfl(pick_byte(d[u][0], (su + 6) & 15), lead + ((su + 6) >> 4), 64);
+                };
+                if constexpr (G >= 16) {
+                    if (!(variant & (1 << 19))) {
+                        // DPP broadcasts of the three window dwords that
+                        // hold packet bytes 0..7 (window dword k is dword
+                        // k & 3 of group lane k >> 2); the ds_bpermute
+                        // exchange (WC_VARIANT bit 19) cost 2048-B netmap
+                        // slots 4 points.
+                        uint32_t w[3];
+#pragma unroll
+                        for (int j = 0; j < 3; ++j) {
+                            const int k = (su >> 2) + j;
+                            const uint32_t mine = pick_dword(d[u][0], k & 3);
+                            // both broadcasts run with every lane active
+                            const uint32_t f0 = group_bcast<G, 0>(mine);
+                            const uint32_t f1 = group_bcast<G, 1>(mine);
+                            w[j] = (k >> 2) ? f1 : f0;
+                        }
+                        const uint32_t sh = 8u * (uint32_t)(su & 3);
+                        const uint32_t x0 = __builtin_amdgcn_alignbit(w[1], w[0], sh); // 0..3
+                        const uint32_t x1 = __builtin_amdgcn_alignbit(w[2], w[1], sh); // 4..7
+                        b0 = x0 & 0xFFu;
+                        b2 = (x0 >> 16) & 0xFFu;
+                        b3 = x0 >> 24;
+                        b6 = (x1 >> 16) & 0xFFu;
+                    } else {
+                        exchange();
+                    }
+                } else {
+                    exchange();
+                }
                 ph = pseudo_hdr(b0, b2, b3, b6);
             }
             const int rs = (int)ph.hl, re = (int)plen[u];
