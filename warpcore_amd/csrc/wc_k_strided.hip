@@ -54,12 +54,6 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
     // WC_VARIANT bit 128 keeps the leader stores (A/B).
     constexpr bool kLaneStore = PPW <= 64;
     const bool lane_store = kLaneStore && !(variant & 128);
-    // U == G (the (4,1,4) shape of 64-B packets): group g takes packets
-    // g U + u instead of u GPW + g, so lane g G + u ends up holding packet
-    // lane's result -- the coalesced store needs no exchange at all.
-    // WC_VARIANT bit 21 keeps the u GPW + g order (A/B).
-    constexpr bool kOwnStore = kLaneStore && U == G && !RAGGED;
-    const bool own_store = kOwnStore && lane_store && !(variant & (1 << 21));
 
     for (uint64_t p0 = wave * PPW; p0 < n; p0 += nwaves * PPW) {
         uint32_t res = 0, res_h = 0;
@@ -73,11 +67,10 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
         // of u - 1 (one 64-bit multiply per wave, not per packet: the
         // address setup runs before the first load).
         const uint64_t a_first = (uint64_t)base + p0 * stride;
-        uint64_t a_u = a_first + (uint64_t)grp * (own_store ? U : 1) * stride;
-        const uint64_t a_step = (uint64_t)(own_store ? 1 : GPW) * stride;
+        uint64_t a_u = a_first + (uint64_t)grp * stride;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-            const uint64_t i = p0 + (own_store ? (uint64_t)grp * U + u : (uint64_t)u * GPW + grp);
+            const uint64_t i = p0 + (uint64_t)u * GPW + grp;
             valid[u] = i < n;
             uint64_t a;
             if constexpr (RAGGED) {
@@ -86,7 +79,7 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
                 plen[u] = lens[ii];
             } else {
                 a = valid[u] ? a_u : a_first;
-                a_u += a_step;
+                a_u += (uint64_t)GPW * stride;
                 plen[u] = len;
             }
             // payload_cksum reads the IPv4 header fields up to byte 19 even
@@ -189,14 +182,6 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
             uint32_t Sh = 0;
             if constexpr (HDR)
                 Sh = group_sum<G>(combine(Eh, Oh, s[u] & 1));
-            if (own_store) {
-                if (gl == u) // this lane is packet p0 + lane
-                    res = fold_not(S);
-                if constexpr (HDR)
-                    if (gl == u)
-                        res_h = ph.v4 ? fold_not(Sh) : 0u;
-                continue;
-            }
             if (lane_store) {
                 // Lane j of the wave takes packet p0 + j's result from its
                 // group (every lane of a group holds the sum).
