@@ -692,7 +692,11 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
         const uint32_t thr = dense ? (uint32_t)(grp_thr & 0xFF) : (uint32_t)(grp_thr >> 8);
         uint32_t Rq = 0;
         bool grouped = false;
-        if (!kSegOnly && thr <= 64u) {
+        // The fused header variant (HDR) leaves the grouped path out: with it
+        // and the gathered path it spilled; the gathered path takes its
+        // uniform tiles (mixed-size ring fused 43 -> 56 %, ragged 1500-B ring
+        // 80.5 -> 79.7 %: profiles/ab_r02_hdr_gather2.log).
+        if (!kSegOnly && !HDR && thr <= 64u) {
             const uint32_t span = grp_span<KIND>(len);
             const uint32_t nchg = valid ? ((uint32_t)(a & 15u) + span + 15u) >> 4 : 0u;
             Rq = (wave_max(nchg) + 15u) >> 4;
@@ -704,12 +708,12 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
         if constexpr (kSegOnly)
             r = seg_tile<UNS, KIND, NT, HDR>(L.seg.pre, L.seg.stage, lane, a, a - A0, len, valid,
                                              T, DenseSrc<UNS, NT>{A0, T, zero}, zero, done, rh);
-        else if (grouped)
+        else if (!HDR && grouped)
             r = grp_tile<UNG, KIND, NT, HDR>(L.grp, lane, a, len, valid, Rq, zero, done, rh);
         else if (dense)
             r = seg_tile<UNS, KIND, NT, HDR>(L.seg.pre, L.seg.stage, lane, a, a - A0, len, valid,
                                              T, DenseSrc<UNS, NT>{A0, T, zero}, zero, done, rh);
-        else if (!STR && !HDR && gather) { // (the fused header variant keeps the flat path: no spills)
+        else if (!STR && gather) {
             // Gathered stream: the tile's packets' chunks in packet order
             // (sparse or unordered tiles -- a netmap ring of mixed sizes).
             const uint32_t span = KIND == WC_KIND_PAYLOAD ? max(len, 20u) : len;
