@@ -440,6 +440,30 @@ def test_payload_strided_netmap_layout(gpu):
         np.testing.assert_array_equal(got, want)
 
 
+@pytest.mark.parametrize("length,stride", [(700, 2048), (1000, 1003), (1500, 1500),
+                                           (1500, 2048), (3000, 3001), (3000, 4096),
+                                           (5000, 5007)])
+def test_payload_strided_group_shapes(gpu, length, stride):
+    """payload_cksum on the group kernel's 16-, 32- and 64-lane shapes, whose
+    header bytes come by DPP broadcast: random header bytes (every version /
+    IHL / length / next-header combination) and well-formed UDP packets, at
+    every start phase (a stride that is not a multiple of 16 moves it packet
+    by packet)."""
+    rng = np.random.default_rng(length + stride)
+    n = 600
+    buf = rng.integers(0, 256, n * stride + 64, dtype=np.uint8)
+    for i in range(0, n, 3):  # every third packet well-formed
+        o = 5 + i * stride
+        pkt, ln = (ipv6_udp if i % 2 else ipv4_udp)(
+            rng.integers(0, 256, length - 28 - (20 if i % 2 else 0), dtype=np.uint8).tobytes(), rng)
+        buf[o:o + ln] = np.frombuffer(pkt, np.uint8)
+    d = dev_u8(buf, gpu)
+    for start in (5, 14):
+        got = host(wc.cksum_strided(d, stride, length, n - 1, kind="payload", byte_offset=start))
+        want = c_oracle.cksum_strided(buf, stride, length, n - 1, kind=1, byte_offset=start)
+        np.testing.assert_array_equal(got, want, err_msg=f"start {start}")
+
+
 @pytest.mark.parametrize("mode", list(RAGGED_MODES))
 @pytest.mark.parametrize("align,lead", [(1, 5), (2, 0)])
 def test_payload_ipv6_wrap(gpu, monkeypatch, align, lead, mode):
