@@ -388,17 +388,28 @@ __device__ __forceinline__ uint32_t group_sum(uint32_t v)
 }
 
 constexpr int kDppRowBcast15Ctl = 0x142; // row_bcast:15 (DPP controls below)
+constexpr int kDppRowShr4Ctl = 0x114;    // row_shr:4
 
-// Lane N of each aligned group of G >= 16 lanes, in every lane of the group:
-// DPP row_newbcast (one 16-lane row), plus row_bcast:15 into the odd rows
-// for G = 32 (lane 15 of rows 0 / 2 then holds their lane N), readlane for
-// G = 64.
+// Lane N of each aligned group of G lanes, in every lane of the group:
+// DPP quad_perm for G = 4; for G = 8 quad_perm and, in the group's second
+// quad, row_shr:4 of it; row_newbcast for G = 16 (one 16-lane row), plus
+// row_bcast:15 into the odd rows for G = 32 (lane 15 of rows 0 / 2 then
+// holds their lane N); readlane for G = 64.  Every lane must be active.
 template <int G, int N>
 __device__ __forceinline__ uint32_t group_bcast(uint32_t v)
 {
-    static_assert(G == 16 || G == 32 || G == 64, "row-based groups");
+    static_assert(G == 4 || G == 8 || G == 16 || G == 32 || G == 64, "group width");
+    static_assert(N >= 0 && N < 4, "source lane within the group's first quad");
     if constexpr (G == 64) {
         return (uint32_t)__builtin_amdgcn_readlane((int)v, N);
+    } else if constexpr (G <= 8) {
+        const uint32_t q = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, N * 0x55, 0xF, 0xF,
+                                                                 false);
+        if constexpr (G == 4)
+            return q;
+        const uint32_t sh = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)q, kDppRowShr4Ctl, 0xF,
+                                                                  0xF, false);
+        return (threadIdx.x & 4) ? sh : q;
     } else {
         const uint32_t t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x150 + N, 0xF, 0xF,
                                                                  false);

@@ -121,13 +121,14 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
                     b3 = __shfl(pick_byte(d[u][0], (su + 3) & 15), lead + ((su + 3) >> 4), 64);
                     b6 = __shfl(pick_byte(d[u][0], (su + 6) & 15), lead + ((su + 6) >> 4), 64);
                 };
-                if constexpr (G >= 16) {
+                {
                     if (!(variant & (1 << 19))) {
                         // DPP broadcasts of the three window dwords that
                         // hold packet bytes 0..7 (window dword k is dword
                         // k & 3 of group lane k >> 2); the ds_bpermute
                         // exchange (WC_VARIANT bit 19) cost 2048-B netmap
-                        // slots 4 points.
+                        // slots 4 points, packed 64-192 B 2-5 points
+                        // (profiles/ab_r02_hdr_dpp.log).
                         uint32_t w[3];
 #pragma unroll
                         for (int j = 0; j < 3; ++j) {
@@ -148,8 +149,6 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
                     } else {
                         exchange();
                     }
-                } else {
-                    exchange();
                 }
                 ph = pseudo_hdr(b0, b2, b3, b6);
             }
