@@ -638,7 +638,11 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     TileLds &L = lds_all[w];
     const uint64_t ntiles = (n + 63) / 64;
     const uint64_t nwaves = (uint64_t)gridDim.x * kFlatWaves;
-    uint64_t tile = xcd_block(variant) * kFlatWaves + w;
+    // XCD super-blocks of 2^13 workgroups (32768 tiles) unless WC_VARIANT
+    // sets the span: +0.5-1 point on C4, the mixed ring and packed 300 B over
+    // the strided kernel's 2^12 (profiles/ab_r02_xcd_span.log).
+    const int xv = (variant & 0xFF00) ? variant : (variant | (13 << 8));
+    uint64_t tile = xcd_block(xv) * kFlatWaves + w;
     uint32_t nbad = 0;
     const uint64_t zero = (uint64_t)(uintptr_t)&kZeroChunk;
 
