@@ -440,6 +440,42 @@ def test_payload_strided_netmap_layout(gpu):
         np.testing.assert_array_equal(got, want)
 
 
+@pytest.mark.parametrize("length", [60, 64, 100, 333, 1000, 1500])
+def test_strided_packed_seg_wild_payload(gpu, monkeypatch, length):
+    """payload_cksum on the seg-only packed strided kernel with random header
+    bytes: IPv4 options up to IHL 15, malformed IHL < 5,
+    IPv6 next_hdr 254 / 255 at odd starts (the uint32 wrap the seg arithmetic
+    can't follow) -- those lanes are recomputed by their own lane
+    (lane_payload_exact), the rest of the tile keeps the seg result."""
+    monkeypatch.setenv("WC_STRIDED_SEG", "2")
+    wc.reload_config()
+    rng = np.random.default_rng(length * 31)
+    n = 700
+    for stride in sorted({length, length + 1}):
+        buf = rng.integers(0, 256, n * stride + 128, dtype=np.uint8)
+        for start in (0, 1, 3):
+            for i in range(n):
+                o = start + i * stride
+                kind = i % 5
+                if kind == 0:              # IPv4 with options: a 60-B header
+                    # (lengths >= 60: a header longer than the packet makes
+                    # the reference read ~4 GiB -- undefined, the oracle
+                    # faults like it)
+                    buf[o] = 0x4F
+                elif kind == 1:
+                    buf[o] = 0x41          # IPv4, malformed IHL 1
+                elif kind == 2:
+                    buf[o] = 0x60          # IPv6, next header near 255
+                    buf[o + 6] = 254 + (i & 1)
+                elif kind == 3:
+                    buf[o] = 0x45
+            d = dev_u8(buf, gpu)
+            got = host(wc.cksum_strided(d, stride, length, n - 1, kind="payload",
+                                        byte_offset=start))
+            want = c_oracle.cksum_strided(buf, stride, length, n - 1, kind=1, byte_offset=start)
+            np.testing.assert_array_equal(got, want, err_msg=f"stride {stride} start {start}")
+
+
 @pytest.mark.parametrize("length,stride", [(700, 2048), (1000, 1003), (1500, 1500),
                                            (1500, 2048), (3000, 3001), (3000, 4096),
                                            (5000, 5007)])

@@ -239,7 +239,12 @@ struct GathSrc {
 // possible uint32 wrap): the caller then takes the exact flat path for the
 // tile.  On a gathered stream a packet's first and last chunks hold other
 // bytes of the same cache lines; they cancel like the gaps of a dense range.
-template <int UNS, int KIND, bool NT, bool HDR, class Src>
+//
+// LANEFIX (payload_cksum on the seg-only packed strided kernel): a lane the
+// seg arithmetic can't take gets done = false on its own, the others keep
+// their result, and the caller recomputes that lane's packet exactly
+// (lane_payload_exact) -- no flat path in that kernel.
+template <int UNS, int KIND, bool NT, bool HDR, class Src, bool LANEFIX = false>
 __device__ __forceinline__ uint16_t seg_tile(uint32_t *pre, u32x4 *stage, int lane, uint64_t a,
                                              uint64_t ra, uint32_t len, bool valid, uint32_t T,
                                              const Src &src, uint64_t zero, bool &done,
@@ -308,7 +313,10 @@ __device__ __forceinline__ uint16_t seg_tile(uint32_t *pre, u32x4 *stage, int la
                        w2 = win_bytes(hs, h1, h2, s, 2);
         const PseudoHdr ph = pseudo_hdr(w0 & 0xFFu, (w0 >> 16) & 0xFFu, w0 >> 24,
                                         (w1 >> 16) & 0xFFu);
-        if (__ballot(valid && !seg_payload_ok(a, len, ph))) {
+        const bool lane_bad = valid && !seg_payload_ok(a, len, ph);
+        if constexpr (LANEFIX) {
+            done = !lane_bad;
+        } else if (__ballot(lane_bad)) {
             done = false;
             return 0;
         }
@@ -331,7 +339,7 @@ __device__ __forceinline__ uint16_t seg_tile(uint32_t *pre, u32x4 *stage, int la
         // IPv4 with hl != 20: the body starts at hl, not 20 -- minus the
         // options [20, hl), or plus [hl, 20) (src/dst then count twice, as in
         // the reference).  <= 40 bytes, <= 4 chunks, loaded by those lanes.
-        const bool corr = ph.v4 && ph.hl != 20u;
+        const bool corr = ph.v4 && ph.hl != 20u && !lane_bad; // (a bad lane's hl may pass len)
         uint32_t cv = 0;
         if (__ballot(valid && corr)) {
             const int clo = (int)min(ph.hl, 20u), chi = (int)max(ph.hl, 20u);
@@ -587,6 +595,24 @@ __device__ __forceinline__ bool seg_dense(int lane, uint64_t a, uint32_t len, bo
     return true;
 }
 
+// payload_cksum of one packet by its own lane, exact byte-lane sums over its
+// chunks (in_cksum.c:140-167, the strided kernel's edge-chunk arithmetic):
+// the seg-only kernel's fallback for a packet whose header is longer than it
+// or whose odd-start sum could wrap -- rare, so a serial loop.
+template <bool NT>
+__device__ __noinline__ uint16_t lane_payload_exact(uint64_t a, uint32_t len)
+{
+    const PseudoHdr ph = hdr_pseudo(load_hdr(a), a);
+    const uint32_t s = (uint32_t)(a & 15u);
+    const uint64_t c0 = a & ~15ull;
+    const uint32_t nch = (s + max(len, 20u) + 15u) >> 4;
+    uint32_t E = 0, O = 0;
+    for (uint32_t k = 0; k < nch; ++k)
+        accum_arith<WC_KIND_PAYLOAD>(load_chunk<NT>(c0 + 16ull * k), 16 * (int)k - (int)s,
+                                     (int)ph.hl, (int)len, ph.v4, E, O);
+    return fold_not(combine(E, O, s & 1u) + ph.special);
+}
+
 } // namespace
 
 // Ragged kernel with both paths: dense tiles stream their byte range
@@ -603,17 +629,18 @@ template <int UN, int UNS, int UNG, int KIND, bool NT, bool STR, bool HDR = fals
 #define WC_SEG_STR_WAVES 4 // the same for packed strided ip_cksum (seg path only)
 #endif
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
-    UNS >= 8 ? 2 : (STR && KIND == WC_KIND_IP ? WC_SEG_STR_WAVES : WC_SEG_WAVES))))
+    UNS >= 8 ? 2 : (STR && !HDR ? WC_SEG_STR_WAVES : WC_SEG_WAVES))))
 k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
             const uint16_t *__restrict__ lens, uint64_t n, uint16_t *__restrict__ out,
             unsigned long long *__restrict__ bad, int grp_thr, int variant, uint64_t stride,
             uint32_t slen, uint16_t *__restrict__ out_hdr, int gather)
 {
     static_assert(!HDR || KIND == WC_KIND_PAYLOAD, "header checksum rides on payload");
-    // Packed strided ip_cksum: every tile is dense and the seg path always
-    // completes, so the other paths (and their registers and LDS) are not
+    // Packed strided batches: every tile is dense and the seg path always
+    // completes (a payload_cksum lane it can't take is recomputed by its own
+    // lane), so the other paths (and their registers and LDS) are not
     // compiled in.
-    constexpr bool kSegOnly = STR && KIND == WC_KIND_IP;
+    constexpr bool kSegOnly = STR && !HDR;
     struct SegLds {
         u32x4 stage[64 * UNS]; // the row group's chunks
         uint32_t pre[64 * UNS];
@@ -709,9 +736,14 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
         }
         bool done = false;
         uint16_t rh = 0;
-        if constexpr (kSegOnly)
-            r = seg_tile<UNS, KIND, NT, HDR>(L.seg.pre, L.seg.stage, lane, a, a - A0, len, valid,
-                                             T, DenseSrc<UNS, NT>{A0, T, zero}, zero, done, rh);
+        if constexpr (kSegOnly) {
+            r = seg_tile<UNS, KIND, NT, HDR, DenseSrc<UNS, NT>, true>(
+                L.seg.pre, L.seg.stage, lane, a, a - A0, len, valid, T,
+                DenseSrc<UNS, NT>{A0, T, zero}, zero, done, rh);
+            if constexpr (KIND == WC_KIND_PAYLOAD)
+                if (!done)
+                    r = lane_payload_exact<NT>(a, len);
+        }
         else if (!HDR && grouped)
             r = grp_tile<UNG, KIND, NT, HDR>(L.grp, lane, a, len, valid, Rq, zero, done, rh);
         else if (dense)
