@@ -11,12 +11,18 @@ path shards by packet with no data-path collective ("scaling": "weak"); ranks
 meet only at the barriers around the timed region and in the max-over-ranks
 time reduction.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4|c5]
-                    [--len L] [--kind ip|payload] [--cpu-seconds S] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+                    [--config c2|c3|c4|c5|slots|zslots|rx] [--len L] [--kind ip|payload]
+                    [--headers] [--fused] [--cpu-seconds S] [--no-cpu-baseline] [--no-c5]
 
---config c5 is SURVEY C5 (strong scaling): 2^28 x 1472 B in total, split
-evenly over the ranks; a rank whose share exceeds its resident window (2^25
-packets = 49 GB) checksums it as several launches over that window.
+Every line also carries a "c5" object: SURVEY C5, the north star's
+strong-scaling curve -- 2^28 x 1472 B in total, split evenly over the N ranks,
+each rank's share checksummed as launches over a resident 2^25-packet (49 GB)
+window -- timed with its own barriers and max over ranks, with sampled
+parity on every rank.  --config c5 makes it the headline instead.
+--fused runs the fused IPv4 header + payload_cksum pass (wc_cksum_ip_udp_*).
+--config rx is the RX verdict pass (wc_rx_verdict_ragged) over a netmap RX
+ring of well-formed UDP frames (2048-B slots, valid IPv4 / IPv6 checksums).
 --config slots is a netmap RX ring drained into one ragged batch
 (backend_netmap.c:379-391): 2^20 IP packets of --len + 28 B (1500 B) in
 2048-B buffers at +14 (eth.h:44-48), through wc_cksum_ragged; use it with
@@ -50,10 +56,16 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="c2",
-                    choices=["c2", "c3", "c4", "c5", "slots", "zslots"])
+                    choices=["c2", "c3", "c4", "c5", "slots", "zslots", "rx"])
     ap.add_argument("--len", type=int, default=1472, help="packet bytes for c3")
     ap.add_argument("--kind", default="ip", choices=["ip", "payload"],
                     help="ip_cksum (default) or payload_cksum per packet")
+    ap.add_argument("--fused", action="store_true",
+                    help="fused IPv4 header checksum + payload_cksum pass (wc_cksum_ip_udp_*; "
+                         "implies --kind payload --headers)")
+    ap.add_argument("--no-c5", action="store_true",
+                    help="skip the C5 strong-scaling leg every line carries by default")
+    ap.add_argument("--c5-steps", type=int, default=3, help="timed steps of the C5 leg")
     ap.add_argument("--headers", action="store_true",
                     help="stamp well-formed IPv4 / IPv6 UDP headers on every packet "
                          "(synth.stamp_udp_headers) instead of random header bytes")
@@ -139,12 +151,16 @@ def dist_setup(args):
 
 
 def make_workload(args, dev, rank, world):
+    """The headline workload of this run on this rank: (step, packets,
+    algorithmic bytes per step, buffer, results, kernel plan, description,
+    config metadata, layout, scaling)."""
     import warpcore_amd as wc
     from warpcore_amd import dist as wdist
     from warpcore_amd import synth
 
     seed = synth.SEED + rank
     kind = args.kind
+    fused = args.fused
     if args.config == "c5":
         L = 1472
         lo, hi = wdist.shard_range(args.total_packets, rank, world)
@@ -167,6 +183,38 @@ def make_workload(args, dev, rank, world):
                 "packet_bytes": L, "layout": "strided", "launches_per_step": launches,
                 "kind": kind}
         return step, share, share * L, buf, out, plan, desc, meta, (L, L), "strong"
+    if args.config in ("rx", "zrx"):
+        # netmap RX ring (backend_netmap.c:379-391): one well-formed UDP
+        # frame per 2048-B slot, valid IPv4 header and UDP checksums; one
+        # step = the RX verdict of every frame (wc_rx_verdict_ragged).
+        slot = 2048
+        if args.config == "rx":
+            n = args.packets
+            ip_lens = np.full(n, args.len + 28, dtype=np.uint16)
+        else:
+            n = 1 << 21 if args.packets == (1 << 20) else args.packets
+            ip_lens = synth.zipf_lengths(n, seed=synth.ZIPF_SEED + rank)
+        buf = torch.empty(n * slot + 64, dtype=torch.uint8, device=dev)
+        wc.synth_fill(buf, seed, nbytes=n * slot)
+        f_off, f_len = synth.make_rx_ring(buf, n, ip_lens, slot=slot)
+        d_off = torch.from_numpy(f_off).to(dev)
+        d_len = torch.from_numpy(f_len).to(dev)
+        out = torch.empty(n, dtype=torch.uint8, device=dev)
+        drops = torch.zeros(1, dtype=torch.int64, device=dev)
+        wc.rx_verdict_ragged(buf, d_off, d_len, out=out, drops=drops)  # validates the layout
+
+        def step():
+            wc.rx_verdict_ragged(buf, d_off, d_len, out=out, check=False, drops=drops)
+
+        nbytes = int(f_len.astype(np.uint64).sum())
+        desc = (f"netmap RX ring: {n} Ethernet frames ({'Zipf 64-1472 B IP, mean ' if args.config == 'zrx' else ''}"
+                f"{nbytes / n:.1f} B) in {slot}-B slots, RX verdict (IPv4 header + UDP "
+                f"checksums, ip4_rx + udp_rx checks) per frame")
+        meta = {"packets_per_gpu": n, "mean_frame_bytes": round(nbytes / n, 2), "slot_bytes": slot,
+                "layout": "ragged", "kind": "rx_verdict"}
+        plan = {"kernel": "k_rx_verdict (header parse + gathered seg stream)",
+                "grid": int((n + 255) // 256)}
+        return step, n, nbytes, buf, out, plan, desc, meta, (f_off, f_len), "weak"
     if args.config in ("c2", "c3"):
         L = 1472 if args.config == "c2" else args.len
         n = args.packets
@@ -177,14 +225,21 @@ def make_workload(args, dev, rank, world):
             synth.stamp_udp_headers(buf, torch.arange(n, device=dev) * L,
                                     torch.full((n,), L, device=dev))
         out = torch.empty(n, dtype=torch.uint16, device=dev)
+        out_hdr = torch.empty(n, dtype=torch.uint16, device=dev) if fused else None
 
         def step():
-            wc.cksum_strided(buf, L, L, n, out=out, kind=kind)
+            if fused:
+                wc.cksum_ip_udp_strided(buf, L, L, n, out_hdr=out_hdr, out=out)
+            else:
+                wc.cksum_strided(buf, L, L, n, out=out, kind=kind)
 
         plan = wc.plan_strided(buf.data_ptr(), L, L, n, kind=kind)
         desc = (f"C2: {n} x {L} B packets, stride {L}, device-resident"
                 if args.config == "c2" else f"C3: {n} x {L} B packets, stride {L}")
         meta = {"packets_per_gpu": n, "packet_bytes": L, "layout": "strided", "kind": kind}
+        if fused:
+            desc += ", fused IPv4 header + payload_cksum pass"
+            meta["out_hdr"] = out_hdr
         return step, n, nbytes, buf, out, plan, desc, meta, (L, L), "weak"
     if args.config in ("slots", "zslots"):
         # netmap RX ring drained into one ragged batch: one IP packet per
@@ -207,11 +262,15 @@ def make_workload(args, dev, rank, world):
         if args.headers:
             synth.stamp_udp_headers(buf, d_off, d_len)
         out = torch.empty(n, dtype=torch.uint16, device=dev)
+        out_hdr = torch.empty(n, dtype=torch.uint16, device=dev) if fused else None
 
         wc.cksum_ragged(buf, d_off, d_len, out=out, kind=kind)  # validates the layout once
 
         def step():
-            wc.cksum_ragged(buf, d_off, d_len, out=out, kind=kind, check=False)
+            if fused:
+                wc.cksum_ip_udp_ragged(buf, d_off, d_len, check=False, out_hdr=out_hdr, out=out)
+            else:
+                wc.cksum_ragged(buf, d_off, d_len, out=out, kind=kind, check=False)
 
         if args.config == "slots":
             desc = (f"netmap RX ring: {n} x {L} B IP packets in {slot}-B slots at +{at}, "
@@ -223,7 +282,10 @@ def make_workload(args, dev, rank, world):
                     f"(mean {nbytes / n:.1f}) in {slot}-B slots at +{at}, ragged batch")
             meta = {"packets_per_gpu": n, "mean_packet_bytes": round(nbytes / n, 2),
                     "slot_bytes": slot, "layout": "ragged", "kind": kind}
-        path = "grouped path" if args.config == "slots" else "gathered-stream path"
+        if fused:
+            desc += ", fused IPv4 header + payload_cksum pass"
+            meta["out_hdr"] = out_hdr
+        path = "grouped path" if args.config == "slots" and not fused else "gathered-stream path"
         plan = {"kernel": f"seg ({path} for these tiles)",
                 "rows_per_group": int(os.environ.get(
                     "WC_GRP_ROWS" if args.config == "slots" else "WC_SEG_ROWS", "4")),
@@ -241,15 +303,22 @@ def make_workload(args, dev, rank, world):
     if args.headers:
         synth.stamp_udp_headers(buf, d_off, d_len)
     out = torch.empty(n, dtype=torch.uint16, device=dev)
+    out_hdr = torch.empty(n, dtype=torch.uint16, device=dev) if fused else None
 
     wc.cksum_ragged(buf, d_off, d_len, out=out, kind=kind)  # validates the layout once
 
     def step():
-        wc.cksum_ragged(buf, d_off, d_len, out=out, kind=kind, check=False)
+        if fused:
+            wc.cksum_ip_udp_ragged(buf, d_off, d_len, check=False, out_hdr=out_hdr, out=out)
+        else:
+            wc.cksum_ragged(buf, d_off, d_len, out=out, kind=kind, check=False)
 
     desc = f"C4: {n} packets, Zipf(s=1) lengths 64-1472 B (mean {nbytes / n:.1f}), packed"
     meta = {"packets_per_gpu": n, "mean_packet_bytes": round(nbytes / n, 2),
             "layout": "ragged", "kind": kind}
+    if fused:
+        desc += ", fused IPv4 header + payload_cksum pass"
+        meta["out_hdr"] = out_hdr
     seg = int(os.environ.get("WC_SEG", "1"))
     if seg != 0:
         plan = {"kernel": "seg (segmented prefix over dense 64-packet tiles, flat fallback)",
@@ -302,22 +371,27 @@ def cpu_baseline(args, buf, shape, nbytes_total):
         desc = f"{n_s} packets x {L} B ({n_s * L / 1e9:.2f} GB, the full batch)"
     else:
         offs, lens = shape
-        n_s = min(offs.size, 1 << 22)
+        n_s = min(offs.size, 1 << 22 if args.config not in ("rx", "zrx") else 1 << 20)
         end = int(offs[n_s - 1]) + max(int(lens[n_s - 1]), 40)
         sample = buf[:end].cpu().numpy()
         o_s, l_s = offs[:n_s], lens[:n_s]
         sbytes = float(l_s.astype(np.uint64).sum())
+        rx = args.config in ("rx", "zrx")
 
         def trial(th):
             t0 = time.perf_counter()
             passes = 0
             while True:
-                c_oracle.cksum_ragged(sample, o_s, l_s, kind=k, threads=th)
+                if rx:
+                    c_oracle.rx_verdict_ragged(sample, o_s, l_s, threads=th)
+                else:
+                    c_oracle.cksum_ragged(sample, o_s, l_s, kind=k, threads=th)
                 passes += 1
                 dt = time.perf_counter() - t0
                 if dt >= per_trial:
                     return passes * sbytes / dt, passes
-        desc = (f"first {n_s} {'Zipf ' if args.config == 'c4' else ''}packets "
+        what = "frames, oracle_rx_verdict" if rx else "packets"
+        desc = (f"first {n_s} {'Zipf ' if args.config in ('c4', 'zslots', 'zrx') else ''}{what} "
                 f"({end / 1e6:.0f} MB)")
     best_all = max(trial(threads)[0] for _ in range(trials))
     best_one = max(trial(1)[0] for _ in range(trials))
@@ -326,6 +400,8 @@ def cpu_baseline(args, buf, shape, nbytes_total):
                      if l.startswith("model name"))
     except (OSError, StopIteration):
         model = "unknown"
+    if args.fused:
+        desc += " (payload_cksum only: the CPU port's header checksum is not timed)"
     return {"value": round(best_all / GIB, 3), "unit": "GiB/s", "cores": threads,
             "kind": "port", "value_1core": round(best_one / GIB, 3), "best_of": trials,
             "cores_visible": visible,
@@ -344,11 +420,18 @@ def last_count(args):
     return share - (share - 1) // win * win
 
 
-def parity_check(args, buf, out, shape, nbytes):
+def parity_check(args, buf, out, shape, nbytes, meta=None):
     """Bit-exact check of the last step's results over EVERY packet of the
     batch against the oracle (run outside the timed region)."""
     from oracle import c_oracle
     k = 1 if args.kind == "payload" else 0
+    if args.config in ("rx", "zrx"):
+        offs, flens = shape
+        hb = buf[: int(offs[-1]) + int(flens[-1])].cpu().numpy()
+        want = c_oracle.rx_verdict_ragged(hb, offs, flens)
+        got = out.cpu().numpy()
+        return {"checked_packets": int(got.size), "mismatches": int((got != want).sum()),
+                "verdicts_ok": int(np.isin(want, (0, 1)).sum())}
     got = out.cpu().numpy().view(np.uint16)
     if args.config in ("c2", "c3", "c5"):
         hb = buf[: got.size * shape[1]].cpu().numpy()
@@ -362,10 +445,90 @@ def parity_check(args, buf, out, shape, nbytes):
         n_chk = got.size if args.config != "c5" else min(got.size, last_count(args))
         want = c_oracle.cksum_strided(hb, stride, L, n_chk, kind=k)
         got = got[:n_chk]
+        offs = np.arange(n_chk, dtype=np.uint64) * np.uint64(stride)
     else:
         offs, lens = shape
         want = c_oracle.cksum_ragged(hb, offs, lens, kind=k)
-    return {"checked_packets": int(got.size), "mismatches": int((got != want).sum())}
+    bad = int((got != want).sum())
+    if meta is not None and meta.get("out_hdr") is not None:
+        # fused pass: the IPv4 header checksums too (ip_cksum(ip, hl), 0 for IPv6)
+        b0 = hb[offs.astype(np.int64)]
+        v4 = (b0 >> 4) == 4
+        hl = np.where(v4, (b0 & 0x0F).astype(np.uint16) * 4, 0).astype(np.uint16)
+        want_h = np.where(v4, c_oracle.cksum_ragged(hb, offs, hl, kind=0), 0).astype(np.uint16)
+        got_h = meta["out_hdr"].cpu().numpy().view(np.uint16)[: got.size]
+        bad += int((got_h != want_h).sum())
+    return {"checked_packets": int(got.size), "mismatches": bad}
+
+
+def c5_leg(args, dev, rank, world, coll_dev):
+    """SURVEY C5 beside the headline (the north star's 1/2/4/8-GPU curve):
+    2^28 x 1472 B in total, split evenly over the ranks (wc_shard_range's
+    split), each rank's share checksummed as launches over a resident
+    2^25-packet (49 GB) window of synthetic bytes.  Timed like the headline
+    (barrier + synchronize on both sides, max over ranks); parity on three
+    sampled 2^16-packet stretches of every rank's window."""
+    import warpcore_amd as wc
+    from oracle import c_oracle
+    from warpcore_amd import dist as wdist
+    from warpcore_amd import synth
+
+    L = 1472
+    lo, hi = wdist.shard_range(args.total_packets, rank, world)
+    share = hi - lo
+    win = min(share, args.window_packets)
+    launches = (share + win - 1) // win
+    counts = [min(win, share - k * win) for k in range(launches)]
+    buf = torch.empty(win * L + 64, dtype=torch.uint8, device=dev)
+    wc.synth_fill(buf, synth.SEED + 1000 + rank, nbytes=win * L)
+    out = torch.empty(win, dtype=torch.uint16, device=dev)
+
+    def step():
+        for c in counts:
+            wc.cksum_strided(buf, L, L, c, out=out, kind="ip")
+
+    step()
+    torch.cuda.synchronize(dev)
+    wdist.barrier(dev)
+    stream = torch.cuda.current_stream(dev)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.c5_steps):
+        step()
+    ev1.record(stream)
+    wdist.barrier(dev)
+    elapsed = wdist.max_over_ranks(time.perf_counter() - t0, coll_dev)
+    kernel_ms = wdist.max_over_ranks(ev0.elapsed_time(ev1) / args.c5_steps / launches, coll_dev)
+    total_bytes = float(args.total_packets) * L * args.c5_steps
+    gbps = total_bytes / elapsed / 1e9
+    # sampled parity: every launch rewrote out[:count] from the same window
+    m = min(1 << 16, counts[-1])
+    bad = 0
+    for s0 in sorted({0, (counts[-1] - m) // 2, counts[-1] - m}):
+        hb = buf[s0 * L:(s0 + m) * L].cpu().numpy()
+        want = c_oracle.cksum_strided(hb, L, L, m, kind=0)
+        bad += int((out[s0:s0 + m].cpu().numpy().view(np.uint16) != want).sum())
+    checked = wdist.sum_over_ranks(3 * m, coll_dev)
+    bad = wdist.sum_over_ranks(bad, coll_dev)
+    del buf, out
+    torch.cuda.empty_cache()
+    return {
+        "workload": (f"SURVEY C5: {args.total_packets} x {L} B = "
+                     f"{args.total_packets * L / 1e9:.1f} GB in total, split evenly over "
+                     f"{world} rank(s): {share} packets per rank as {launches} launch(es) over "
+                     f"a resident {win}-packet window"),
+        "scaling": "strong", "n_gpus": world, "steps": args.c5_steps,
+        "ms_per_step": round(elapsed / args.c5_steps * 1e3, 3),
+        "value": round(total_bytes / elapsed / GIB, 2), "unit": "GiB/s",
+        "GBps": round(gbps, 1),
+        "frac_job": round(gbps / (world * HBM_PEAK_GBPS), 4),
+        "kernel_ms_avg_max_rank": round(kernel_ms, 4),
+        "frac_kernel": round(counts[0] * L / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+        "parity": {"checked_packets": checked, "mismatches": bad,
+                   "sample": "3 x 2^16 packets per rank (start, middle, end of the window)"},
+    }
 
 
 def main():
@@ -378,6 +541,8 @@ def main():
     dev = torch.device("cuda", local)
     import warpcore_amd as wc
     wc.gpu_init(local)
+    if args.fused:  # the fused pass is payload_cksum over real UDP headers
+        args.kind, args.headers = "payload", True
 
     step, n, nbytes, buf, out, plan, desc, meta, shape, scaling = make_workload(
         args, dev, rank, world)
@@ -413,15 +578,17 @@ def main():
     achieved = nbytes / (kernel_ms_max * 1e-3) / 1e9
     frac_job = value * GIB / 1e9 / (world * HBM_PEAK_GBPS)
 
-    parity = parity_check(args, buf, out, shape, nbytes)
-    parity["checked_packets"] = wdist.sum_over_ranks(parity["checked_packets"], coll_dev)
-    parity["mismatches"] = wdist.sum_over_ranks(parity["mismatches"], coll_dev)
+    parity = parity_check(args, buf, out, shape, nbytes, meta)
+    meta.pop("out_hdr", None)
+    for key in list(parity):
+        if isinstance(parity[key], int):
+            parity[key] = wdist.sum_over_ranks(parity[key], coll_dev)
 
     # after the timed region the ranks exchange their 2-byte
     # results (RCCL all-gather over xGMI; host tensors for the gloo
     # rehearsal), so every rank holds the whole job's results in packet order.
     gather = None
-    if (world > 1 or wdist._pg_active()) and out.numel() == n:
+    if (world > 1 or wdist._pg_active()) and out.numel() == n and out.element_size() == 2:
         src = out.view(torch.int16)
         if coll_dev.type != "cuda":
             src = src.cpu()
@@ -442,10 +609,12 @@ def main():
     try:
         tf = json.loads(Path(args.traffic_file).read_text())
         key = f"{args.config}:{meta.get('packet_bytes', 'zipf')}"
-        if args.kind != "ip":
+        if args.kind != "ip" and args.config not in ("rx", "zrx"):
             key += f":{args.kind}"
-        if args.headers:
+        if args.headers and args.config not in ("rx", "zrx"):
             key += ":headers"
+        if args.fused:
+            key += ":fused"
         if key in tf:
             traffic = tf[key]["hbm_bytes_per_launch"]
             traffic_source = (f"{os.path.relpath(args.traffic_file, ROOT)} [{key}] "
@@ -454,9 +623,17 @@ def main():
     except (OSError, ValueError, KeyError):
         traffic = None
 
+    # The CPU baseline at every N (rank 0's host cores, its own batch), then
+    # the C5 strong-scaling leg -- both after the headline's timed region.
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, buf, shape, nbytes)
+    wdist.barrier(dev)
+    c5 = None
+    if not args.no_c5 and args.config != "c5":
+        del step, buf, out
+        torch.cuda.empty_cache()
+        c5 = c5_leg(args, dev, rank, world, coll_dev)
 
     if rank == 0:
         line = {
@@ -473,7 +650,9 @@ def main():
             "dtype": "u8",
             "data": "synthetic: splitmix64 payload bytes generated on device (wc_synth_fill)"
                     + ("; well-formed IPv4 (IHL 5) / IPv6 UDP headers stamped 2:1"
-                       if args.headers else ""),
+                       if args.headers else "")
+                    + ("; Ethernet frames with valid IPv4 header and UDP checksums"
+                       if args.config in ("rx", "zrx") else ""),
             "config": {"workload": desc, **meta, "parallelism": f"packet-shard x{world}",
                        "kernel_shape": plan, "payload_GBps": round(value * GIB / 1e9, 1)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
@@ -485,6 +664,7 @@ def main():
                          "kernel_ms_avg_max_rank": round(kernel_ms_max, 5)},
             "cpu_baseline": cpu,
             "parity": parity,
+            "c5": c5,
         }
         if gather is not None:
             line["results_allgather"] = gather

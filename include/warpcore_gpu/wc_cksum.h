@@ -91,6 +91,45 @@ int wc_cksum_ip_udp_ragged(const void *d_base, const uint64_t *d_off,
                            const uint16_t *d_len, uint64_t n, uint16_t *d_out_ip_hdr,
                            uint16_t *d_out_payload, void *stream);
 
+/* --- RX verdict: the reference's RX checks, decided on the device -------- */
+
+/* What the reference's RX path decides for one Ethernet frame from its
+ * checksums and header format: eth_rx (eth.c:77-87) -> ip4_rx
+ * (ip4.c:95-138) / ip6_rx (ip6.c:95-110) -> udp_rx (udp.c:99-139).  The
+ * checks run in the reference's order; the first that fails names the code.
+ * Engine state -- MAC and IP address filters (eth.c:65-74, ip4.c:103-108,
+ * ip6.c:101-104), bound sockets -- is not part of the verdict. */
+enum wc_rx_verdict {
+    WC_RX_OK = 0,            /* UDP, checksum verified (udp.c:134): deliver */
+    WC_RX_OK_NO_CKSUM = 1,   /* UDP checksum field 0: accepted unverified (udp.c:132) */
+    WC_RX_BAD_IP_CKSUM = 2,  /* ip_cksum(ip, hl) != 0 (ip4.c:110-115): drop */
+    WC_RX_BAD_UDP_CKSUM = 3, /* payload_cksum(ip, udp_len + hl) != 0 (udp.c:134-139): drop */
+    WC_RX_SHORT = 4,         /* IP payload shorter than a UDP header (udp.c:121-124): drop */
+    WC_RX_FRAGMENT = 5,      /* IPv4 fragment offset != 0 (ip4.c:122-126): drop */
+    WC_RX_BAD_VERSION = 6,   /* version nibble != the EtherType's (ip4.c:95-98, ip6.c:95-99): drop */
+    WC_RX_NOT_UDP = 7,       /* IPv4 / IPv6, another protocol (ICMP, ...): the host's (ip4.c:129-137) */
+    WC_RX_NOT_IP = 8,        /* EtherType neither IPv4 nor IPv6 (ARP, ...): the host's (eth.c:77-87) */
+    WC_RX_TRUNCATED = 9,     /* a byte the reference reads lies past the frame: drop */
+};
+#define WC_RX_IS_DROP(v) \
+    ((v) != WC_RX_OK && (v) != WC_RX_OK_NO_CKSUM && (v) != WC_RX_NOT_UDP && (v) != WC_RX_NOT_IP)
+
+/* Frame i is the Ethernet frame [d_base + d_off[i], + d_frame_len[i]) -- a
+ * netmap slot buffer and its slot length (backend_netmap.c:379-391), or any
+ * batch of frames; no header is parsed on the host.  d_verdict[i] receives
+ * its enum wc_rx_verdict code (uint8); *d_drops (device uint64, optional,
+ * accumulated) counts the frames whose code is a drop (WC_RX_IS_DROP).  No
+ * byte outside a frame is read: what the reference would read past the frame
+ * (its neighbouring buffers) yields WC_RX_TRUNCATED. */
+int wc_rx_verdict_ragged(const void *d_base, const uint64_t *d_off, const uint16_t *d_frame_len,
+                         uint64_t n, uint8_t *d_verdict, uint64_t *d_drops, void *stream);
+
+/* Host-memory frames (the netmap buffer area w->mem, ideally registered with
+ * wc_host_register): synchronous; *h_drops (optional) = the drop count. */
+int wc_rx_verdict_host(const void *h_base, uint64_t h_bytes, const uint64_t *h_off,
+                       const uint16_t *h_frame_len, uint64_t n, uint8_t *h_verdict,
+                       uint64_t *h_drops);
+
 /* --- host-memory batch (end-to-end: pinned H2D, kernel, D2H) ------------- */
 
 /* Same as wc_cksum_ragged, but every buffer is host memory: packet i is
@@ -107,7 +146,8 @@ int wc_cksum_host(const void *h_base, uint64_t h_bytes, const uint64_t *h_off,
                   const uint16_t *h_len, uint64_t n, uint16_t *h_out, int kind);
 
 /* Page-lock a host region (e.g. the netmap buffer area w->mem,
- * backend_netmap.c:149-151) so wc_cksum_host can DMA from it directly. */
+ * backend_netmap.c:149-151) so wc_cksum_host can DMA from it directly.
+ * Registering the same base again is a no-op (a larger size re-registers). */
 int wc_host_register(void *h_ptr, uint64_t bytes);
 int wc_host_unregister(void *h_ptr);
 
@@ -170,8 +210,9 @@ int wc_gather_results_multi(uint16_t *const *d_shard_out, const uint64_t *n,
  * (staging ring, streams).  Called implicitly by every entry point with
  * device -1 ("current device"); calling it explicitly is optional. */
 int wc_gpu_init(int device);
-/* Release the scratch created by wc_gpu_init, and every page-lock taken by
- * wc_host_register (register again after a re-init). */
+/* Release the scratch created by wc_gpu_init / wc_gpu_init_multi and the
+ * RCCL communicators.  Page-locks taken with wc_host_register are the
+ * caller's and stay until wc_host_unregister. */
 int wc_gpu_fini(void);
 
 /* The WC_* tuning environment (kernel shapes, path choices) is

@@ -37,6 +37,8 @@ def load() -> ctypes.CDLL:
                                          [vp, u64, u16, u64, vp, i, i, ctypes.c_double,
                                           ctypes.POINTER(u64)]),
                 "oracle_synth_fill": (None, [vp, u64, u64]),
+                "oracle_rx_verdict": (i, [vp, u16]),
+                "oracle_rx_verdict_ragged": (None, [vp, vp, vp, u64, vp, i]),
             }
             for name, (res, args) in sig.items():
                 fn = getattr(lib, name)
@@ -91,6 +93,29 @@ def cksum_ragged(buf: np.ndarray, off: np.ndarray, lens: np.ndarray, kind: int =
     out = np.empty(off.size, dtype=np.uint16)
     load().oracle_cksum_ragged(a.ctypes.data, off.ctypes.data, lens.ctypes.data, off.size,
                                out.ctypes.data, kind, threads or default_threads())
+    return out
+
+
+def rx_verdict(frame, flen=None) -> int:
+    a = _u8(np.frombuffer(bytes(frame), dtype=np.uint8) if not isinstance(frame, np.ndarray)
+            else frame)
+    flen = a.size if flen is None else flen
+    if flen > a.size:
+        raise ValueError("frame shorter than flen")
+    return int(load().oracle_rx_verdict(a.ctypes.data, flen))
+
+
+def rx_verdict_ragged(buf: np.ndarray, off: np.ndarray, flen: np.ndarray,
+                      threads: int | None = None) -> np.ndarray:
+    """RX verdicts (uint8 codes) of the frames buf[off[i] : off[i] + flen[i]]."""
+    a = _u8(buf)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    flen = np.ascontiguousarray(flen, dtype=np.uint16)
+    if off.size and int((off + flen).max()) > a.size:
+        raise ValueError("a frame runs past the buffer")
+    out = np.empty(off.size, dtype=np.uint8)
+    load().oracle_rx_verdict_ragged(a.ctypes.data, off.ctypes.data, flen.ctypes.data, off.size,
+                                    out.ctypes.data, threads or default_threads())
     return out
 
 

@@ -166,6 +166,117 @@ void oracle_cksum_ragged(const uint8_t *base, const uint64_t *off,
     run_batch(p, n, threads);
 }
 
+/* ------------------------------------------------------------------------- */
+/* RX verdict (the checksum and format decisions of the reference's RX path). */
+
+enum {
+    RX_OK = 0, RX_OK_NO_CKSUM = 1, RX_BAD_IP_CKSUM = 2, RX_BAD_UDP_CKSUM = 3,
+    RX_SHORT = 4, RX_FRAGMENT = 5, RX_BAD_VERSION = 6, RX_NOT_UDP = 7, RX_NOT_IP = 8,
+    RX_TRUNCATED = 9,
+};
+
+static inline uint16_t be16_at(const uint8_t *p) { return (uint16_t)((p[0] << 8) | p[1]); }
+
+int oracle_rx_verdict(const uint8_t *f, uint16_t flen)
+{
+    /* eth_rx (eth.c:77-87): dispatch on the EtherType @12 (eth.h:44-53). */
+    if (flen < 14)
+        return RX_TRUNCATED;
+    const uint16_t type = be16_at(f + 12);
+    if (type != 0x0800 && type != 0x86DD)
+        return RX_NOT_IP; /* ARP and the rest: the engine's business */
+    const uint8_t *ip = f + 14;
+    const uint32_t room = (uint32_t)flen - 14; /* IP bytes inside the frame */
+    if (room < 1)
+        return RX_TRUNCATED;
+    const int v4 = type == 0x0800;
+    /* ip4_rx / ip6_rx: version nibble (ip4.c:95-98, ip6.c:95-99, ip4.h:75-79) */
+    if ((ip[0] >> 4) != (v4 ? 4 : 6))
+        return RX_BAD_VERSION;
+    uint32_t hl, ip_plen, proto;
+    if (v4) {
+        hl = (uint32_t)(ip[0] & 0x0Fu) * 4u; /* ip4_hl, ip4.h:88-92 */
+        /* ip4_rx and udp_rx read the fixed header (len @2, off @6, p @9,
+         * src/dst @12..19) and ip_cksum reads [0, hl). */
+        if (room < (hl > 20 ? hl : 20))
+            return RX_TRUNCATED;
+        if (oracle_ip_cksum(ip, (uint16_t)hl) != 0) /* ip4.c:110-115 */
+            return RX_BAD_IP_CKSUM;
+        /* ip->off & IP4_OFFMASK (0xff1f in network order, ip4.h:49): the
+         * 13-bit fragment offset; the MF flag alone passes (ip4.c:122-126). */
+        if ((ip[6] & 0x1Fu) || ip[7])
+            return RX_FRAGMENT;
+        proto = ip[9];
+        /* udp.c:104: uint16 arithmetic, wraps when len < hl */
+        ip_plen = (uint16_t)(be16_at(ip + 2) - hl);
+    } else {
+        hl = 40; /* sizeof(struct ip6_hdr), udp.c:115 */
+        if (room < 40)
+            return RX_TRUNCATED;
+        proto = ip[6];          /* next_hdr, ip6.c:105 */
+        ip_plen = be16_at(ip + 4); /* udp.c:116 */
+    }
+    if (proto != 17) /* IP_P_UDP: ICMP and the rest go elsewhere */
+        return RX_NOT_UDP;
+    if (ip_plen < 8) /* udp.c:121-124 */
+        return RX_SHORT;
+    if (room < hl + 8) /* the UDP header (udp.h:41-46) at ip + hl */
+        return RX_TRUNCATED;
+    const uint8_t *udp = ip + hl;
+    const uint32_t ulen = be16_at(udp + 4);
+    const uint32_t udp_len = ulen < ip_plen ? ulen : ip_plen; /* udp.c:126 */
+    if (udp[6] == 0 && udp[7] == 0) /* udp.c:132: no checksum, accepted */
+        return RX_OK_NO_CKSUM;
+    /* payload_cksum(ip, udp_len + hl) reads [0, max(len, 20)) -- the length
+     * is passed as a uint16, and any value past 65535 would wrap below hl
+     * (a ~4 GiB read in the reference): both are past the frame here. */
+    const uint32_t plen = udp_len + hl;
+    if (room < (plen > 20 ? plen : 20))
+        return RX_TRUNCATED;
+    return oracle_payload_cksum(ip, (uint16_t)plen) != 0 ? RX_BAD_UDP_CKSUM : RX_OK;
+}
+
+struct rx_shard {
+    const uint8_t *base;
+    const uint64_t *off;
+    const uint16_t *flen;
+    uint64_t lo, hi;
+    uint8_t *out;
+};
+
+static void *run_rx_shard(void *arg)
+{
+    const struct rx_shard *s = arg;
+    for (uint64_t i = s->lo; i < s->hi; i++)
+        s->out[i] = (uint8_t)oracle_rx_verdict(s->base + s->off[i], s->flen[i]);
+    return NULL;
+}
+
+void oracle_rx_verdict_ragged(const uint8_t *base, const uint64_t *off, const uint16_t *flen,
+                              uint64_t n, uint8_t *out, int threads)
+{
+    if (threads < 1)
+        threads = 1;
+    if ((uint64_t)threads > n)
+        threads = n ? (int)n : 1;
+    if (threads > 256)
+        threads = 256;
+    pthread_t tid[256];
+    struct rx_shard sh[256];
+    for (int t = 0; t < threads; t++) {
+        sh[t] = (struct rx_shard){base, off, flen, n * (uint64_t)t / (uint64_t)threads,
+                                  n * (uint64_t)(t + 1) / (uint64_t)threads, out};
+        if (threads > 1)
+            pthread_create(&tid[t], NULL, run_rx_shard, &sh[t]);
+    }
+    if (threads == 1) {
+        run_rx_shard(&sh[0]);
+        return;
+    }
+    for (int t = 0; t < threads; t++)
+        pthread_join(tid[t], NULL);
+}
+
 static double now_s(void)
 {
     struct timespec ts;

@@ -63,6 +63,16 @@ double oracle_bench_strided(const uint8_t *base, uint64_t stride, uint16_t len,
                             uint64_t n, uint16_t *out, int kind, int threads,
                             double min_seconds, uint64_t *passes);
 
+/* RX verdict of one Ethernet frame of `flen` bytes: what the reference's RX
+ * path decides from checksums and header format (eth_rx eth.c:52-88 ->
+ * ip4_rx ip4.c:87-138 / ip6_rx ip6.c:83-111 -> udp_rx udp.c:80-139), codes
+ * as in include/warpcore_gpu/wc_cksum.h (enum wc_rx_verdict).  Reads only
+ * bytes [0, flen).  Engine state (MAC / address filters, bound sockets) is
+ * the caller's and not part of the verdict. */
+int oracle_rx_verdict(const uint8_t *frame, uint16_t flen);
+void oracle_rx_verdict_ragged(const uint8_t *base, const uint64_t *off, const uint16_t *flen,
+                              uint64_t n, uint8_t *out, int threads);
+
 /* Counter-based synthetic bytes: little-endian 8-byte word k of the stream is
  * splitmix64 output number k for state `seed` (see warpcore_amd synth kernel,
  * which must produce identical bytes). */

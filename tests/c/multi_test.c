@@ -141,6 +141,18 @@ int main(int argc, char **argv)
     CHECK(wc_host_unregister(buf) == WC_OK);
     CHECK(host_multi_case("4 shards on GPU 0", buf, bytes, off, len, n, want_ip, want_pl,
                           got) == 0);
+    /* an invalid device list is refused before the shard set changes, and
+     * the old set keeps working (no half-built executors) */
+    {
+        const int bad[2] = {0, 4096};
+        CHECK(wc_gpu_init_multi(2, bad) == WC_EINVAL);
+        CHECK(wc_gpu_multi_count() == 4);
+        CHECK(host_multi_case("after a refused init", buf, bytes, off, len, n, want_ip, want_pl,
+                              got) == 0);
+        const int neg[1] = {-1};
+        CHECK(wc_gpu_init_multi(1, neg) == WC_EINVAL);
+        CHECK(wc_gpu_multi_count() == 4);
+    }
     /* a shard device listed twice cannot join an RCCL communicator twice */
     {
         uint16_t *dummy[4] = {0};

@@ -86,6 +86,112 @@ def random_packets(rng: np.random.Generator, count: int, max_payload: int = 1472
     return pkts
 
 
+def _u16le_store(b: bytearray, at: int, v: int) -> None:
+    b[at] = v & 0xFF
+    b[at + 1] = (v >> 8) & 0xFF
+
+
+def finish_udp(pkt: bytes, zero_udp: bool = False) -> bytes:
+    """TX side of the reference on an IP packet built above: the IPv4 header
+    checksum over [0, hl) with the field 0 (ip4.c:184-186), then the UDP
+    checksum with the field 0 (udp.c:209-213), both stored raw.  A computed
+    UDP checksum of 0 is sent as 0, i.e. "no checksum" (udp.c:212)."""
+    from oracle import py_oracle  # test infrastructure
+    b = bytearray(pkt)
+    v4 = b[0] >> 4 == 4
+    hl = (b[0] & 0x0F) * 4 if v4 else 40
+    if v4:
+        b[10:12] = b"\x00\x00"
+        _u16le_store(b, 10, py_oracle.ip_cksum(bytes(b[:hl])))
+    o = hl + 6
+    b[o:o + 2] = b"\x00\x00"
+    if not zero_udp:
+        ln = hl + ((b[hl + 4] << 8) | b[hl + 5])
+        _u16le_store(b, o, py_oracle.payload_cksum(bytes(b), min(ln, len(b))))
+    return bytes(b)
+
+
+def eth_frame(ip_pkt: bytes, rng: np.random.Generator, etype: int = 0x0800) -> bytes:
+    """Ethernet II frame around an IP packet (eth.h:44-53): random MACs."""
+    return rng.integers(0, 256, 12, dtype=np.uint8).tobytes() + _u16be(etype) + ip_pkt
+
+
+RX_CASES = ("ok4", "ok6", "ok4opt", "nocksum", "badudp", "badip", "frag", "mf", "short", "icmp4",
+            "icmp6", "arp", "badver", "trunc", "ulen_big", "ulen_small", "totlen_wrap",
+            "ihl_small", "garbage", "tiny")
+
+
+def rx_frame(rng: np.random.Generator, case: str, max_payload: int = 1472) -> tuple[bytes, int]:
+    """One Ethernet frame of an RX ring exercising `case` of the reference's
+    RX checks (ip4.c:95-138, ip6.c:95-110, udp.c:99-139); returns (bytes,
+    frame length), the length possibly shorter than the bytes (a truncated
+    slot: what lies past it is not part of the frame)."""
+    plen = int(rng.integers(0, max_payload + 1))
+    payload = rng.integers(0, 256, plen, dtype=np.uint8).tobytes()
+    v6 = case in ("ok6", "icmp6") or (case in ("nocksum", "badudp", "short", "trunc",
+                                               "ulen_big", "ulen_small") and rng.random() < 0.4)
+    ihl = int(rng.integers(6, 16)) if case == "ok4opt" else 5
+    if case == "arp":
+        fr = eth_frame(rng.integers(0, 256, 28, dtype=np.uint8).tobytes(), rng, 0x0806)
+        return fr, len(fr)
+    if case == "garbage":
+        body = bytearray(rng.integers(0, 256, int(rng.integers(1, 200)), dtype=np.uint8).tobytes())
+        et = 0x0800 if rng.random() < 0.5 else 0x86DD
+        body[0] = ((4 if et == 0x0800 else 6) << 4) | (body[0] & 0x0F)
+        if rng.random() < 0.5 and len(body) > 9:
+            body[6 if et == 0x86DD else 9] = 17
+        fr = eth_frame(bytes(body), rng, et)
+        return fr, len(fr)
+    if case == "tiny":
+        fr = rng.integers(0, 256, int(rng.integers(0, 40)), dtype=np.uint8).tobytes()
+        if len(fr) >= 14 and rng.random() < 0.7:
+            fr = fr[:12] + _u16be(0x0800 if rng.random() < 0.5 else 0x86DD) + fr[14:]
+        return fr, len(fr)
+    if v6:
+        pkt, _ = ipv6_udp(payload, rng, next_hdr=58 if case == "icmp6" else 17)
+    else:
+        pkt, _ = ipv4_udp(payload, rng, ihl=ihl, proto=1 if case == "icmp4" else 17)
+    b = bytearray(pkt)
+    hl = 40 if v6 else ihl * 4
+    if case == "short":  # IP payload < 8 (udp.c:121-124)
+        if v6:
+            b[4:6] = _u16be(int(rng.integers(0, 8)))
+        else:
+            b[2:4] = _u16be(hl + int(rng.integers(0, 8)))
+    if case == "ulen_big":  # udp->len > ip_plen: MIN() takes ip_plen (udp.c:126)
+        b[hl + 4:hl + 6] = _u16be(int(rng.integers(len(b) - hl + 1, 65536)))
+    if case == "ulen_small":  # udp->len < 8 or shorter than the datagram
+        b[hl + 4:hl + 6] = _u16be(int(rng.integers(0, max(9, len(b) - hl))))
+    if case == "totlen_wrap":  # IPv4 total length < hl: ip_plen wraps (udp.c:104)
+        b[2:4] = _u16be(int(rng.integers(0, hl)))
+    if case == "frag":
+        b[6] = (b[6] & 0xE0) | int(rng.integers(0, 32))
+        b[7] = int(rng.integers(1 if b[6] & 0x1F == 0 else 0, 256))
+    if case == "mf":  # More Fragments alone is not in IP4_OFFMASK (ip4.h:49)
+        b[6], b[7] = 0x20, 0x00
+    if case == "ihl_small":  # malformed IHL < 5 with a valid header checksum
+        b[0] = 0x40 | int(rng.integers(0, 5))
+    pkt = finish_udp(bytes(b), zero_udp=(case == "nocksum"))
+    b = bytearray(pkt)
+    if case == "badudp":
+        k = int(rng.integers(hl, len(b)))
+        b[k] ^= 1 << int(rng.integers(0, 8))
+    if case == "badip":
+        b[int(rng.integers(0, hl))] ^= 1 << int(rng.integers(0, 8))
+    if case == "badver":
+        b[0] = (int(rng.choice([0, 1, 5, 7, 15] + ([4] if v6 else [6]))) << 4) | (b[0] & 0x0F)
+    fr = eth_frame(bytes(b), rng, 0x86DD if v6 else 0x0800)
+    flen = len(fr)
+    if case == "trunc":
+        flen = int(rng.integers(14, len(fr)))
+    return fr, flen
+
+
+def rx_ring(rng: np.random.Generator, count: int, cases=RX_CASES, max_payload: int = 1472):
+    """`count` frames cycling through `cases`: list of (bytes, frame length)."""
+    return [rx_frame(rng, cases[i % len(cases)], max_payload) for i in range(count)]
+
+
 def pack(pkts: list[tuple[bytes, int]], align: int = 1, lead: int = 0):
     """Concatenate packets (each start rounded up to `align`, after `lead`
     bytes) -> (buffer, offsets uint64, lens uint16)."""

@@ -50,3 +50,28 @@ def test_code_object_targets_gfx950_only():
     blob = _build.build_lib().read_bytes()
     targets = set(re.findall(rb"amdgcn-amd-amdhsa-[-a-z0-9:+]*gfx[0-9a-z]+", blob))
     assert targets == {b"amdgcn-amd-amdhsa--gfx950"}
+
+
+def test_production_library_has_no_tuning_paths():
+    """WC_VARIANT / WC_DIAG_NOLOAD (result-dropping A/B knobs) exist only in
+    the -DWC_TUNING build: the shipped library carries no no-load kernel,
+    and its version string says it is not the tuning build."""
+    lib = _build.build_lib()
+    syms = subprocess.run(["nm", "-DC", str(lib)], check=True, capture_output=True,
+                          text=True).stdout
+    flat = re.findall(r"wc::k_cksum_flat<(\d+), (\d+), (\w+), (\w+), (\w+), (\d+)>", syms)
+    assert flat and not any(noload == "true" for *_, noload, _pk in flat)
+    assert "TUNING" not in _lib.load().wc_version().decode()
+    text = (ROOT / "warpcore_amd" / "csrc" / "wc_cksum_api.cpp").read_text()
+    # the env reads of both knobs sit inside #ifdef WC_TUNING
+    block = text[text.index("#ifdef WC_TUNING"):text.index("#endif", text.index("#ifdef WC_TUNING"))]
+    assert '"WC_VARIANT"' in block and '"WC_DIAG_NOLOAD"' in block
+    assert text.count('"WC_VARIANT"') == 1 and text.count('"WC_DIAG_NOLOAD"') == 1
+
+
+def test_build_staleness_is_a_source_hash():
+    """A copied tree keeps its binary only if the sources hash the same."""
+    _build.build_lib()
+    assert _build.lib_is_current()
+    stamp = _build._stamp(_build.LIB)
+    assert stamp.read_text().strip() == _build._src_hash(_build.HIP_DEPS, _build.lib_flags())

@@ -23,9 +23,14 @@ def _last_json(out: str) -> dict:
     return json.loads(lines[0])
 
 
+SMALL_C5 = ["--total-packets", str(1 << 22), "--window-packets", str(1 << 20)]
+
+
 def test_bench_one_gpu_line(gpu):
+    """The driver's line at reduced size: C2 headline, CPU baseline and the C5
+    strong-scaling leg (2^22 packets over a 2^20 window here)."""
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--steps", "5", "--warmup", "1",
-                        "--packets", "65536", "--cpu-seconds", "0.5"],
+                        "--packets", "65536", "--cpu-seconds", "0.5", *SMALL_C5],
                        capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     line = _last_json(r.stdout)
@@ -34,6 +39,11 @@ def test_bench_one_gpu_line(gpu):
     assert line["roofline"]["bound"] == "hbm" and 0 < line["roofline"]["frac"] < 1.5
     assert line["cpu_baseline"]["kind"] == "port" and line["cpu_baseline"]["cores"] >= 1
     assert line["parity"]["mismatches"] == 0
+    c5 = line["c5"]
+    assert c5["scaling"] == "strong" and c5["n_gpus"] == 1 and c5["value"] > 0
+    assert "4 launch(es)" in c5["workload"] and 0 < c5["frac_job"] < 1.5
+    assert c5["parity"] == {"checked_packets": 3 << 16, "mismatches": 0,
+                            "sample": c5["parity"]["sample"]}
 
 
 def test_bench_two_ranks_rehearsal(gpu):
@@ -45,12 +55,16 @@ def test_bench_two_ranks_rehearsal(gpu):
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
                         "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
                         "--master-port", str(port), str(ROOT / "bench.py"), "--gpus", "2",
-                        "--steps", "5", "--warmup", "1", "--packets", "65536"],
+                        "--steps", "5", "--warmup", "1", "--packets", "65536",
+                        "--cpu-seconds", "0.3", *SMALL_C5],
                        capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     line = _last_json(r.stdout)
     assert line["n_gpus"] == 2 and line["scaling"] == "weak"
-    assert line["cpu_baseline"] is None
+    assert line["cpu_baseline"]["cores"] >= 1  # rank 0's host cores, at every N
+    c5 = line["c5"]  # the strong split: each of 2 ranks takes 2^21 as 2 launches
+    assert c5["n_gpus"] == 2 and "2097152 packets per rank as 2 launch(es)" in c5["workload"]
+    assert c5["parity"]["checked_packets"] == 2 * (3 << 16) and c5["parity"]["mismatches"] == 0
     assert line["parity"] == {"checked_packets": 2 * 65536, "mismatches": 0}
     assert line["results_allgather"]["ranks_mismatched"] == 0
     assert line["results_allgather"]["bytes_per_rank"] == 2 * 65536
@@ -61,12 +75,17 @@ def test_bench_two_ranks_rehearsal(gpu):
                                    "--headers"],
                                   ["--config", "slots", "--packets", "65536", "--kind", "payload",
                                    "--headers"],
-                                  ["--config", "c2", "--packets", "65536", "--kind", "payload"]])
+                                  ["--config", "c2", "--packets", "65536", "--kind", "payload"],
+                                  ["--config", "c4", "--packets", "200000", "--fused"],
+                                  ["--config", "zslots", "--packets", "100000", "--fused"],
+                                  ["--config", "c2", "--packets", "65536", "--fused"],
+                                  ["--config", "rx", "--packets", "65536"],
+                                  ["--config", "zrx", "--packets", "100000"]])
 def test_bench_other_configs(gpu, args):
     """The secondary bench lines (C4, payload_cksum, the netmap RX-ring layout)
     stay runnable and bit-exact."""
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--steps", "3", "--warmup", "1",
-                        "--cpu-seconds", "0.2", *args],
+                        "--cpu-seconds", "0.2", "--no-c5", *args],
                        capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     line = _last_json(r.stdout)
@@ -81,7 +100,8 @@ def test_bench_spawns_ranks_without_torchrun(gpu):
            if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
     env["WC_DIST_BACKEND"] = "gloo"
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2",
-                        "--steps", "5", "--warmup", "1", "--packets", "65536"],
+                        "--steps", "5", "--warmup", "1", "--packets", "65536", "--no-c5",
+                        "--no-cpu-baseline"],
                        capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     line = _last_json(r.stdout)
@@ -137,9 +157,52 @@ def test_bench_rccl_code_path_one_rank(gpu):
     env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
                MASTER_PORT=str(port), WC_DIST_FORCE_PG="1", WC_DIST_BACKEND="nccl")
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "1", "--steps", "5",
-                        "--warmup", "1", "--packets", "65536", "--no-cpu-baseline"],
+                        "--warmup", "1", "--packets", "65536", "--no-cpu-baseline",
+                        *SMALL_C5],
                        capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     line = _last_json(r.stdout)
     assert line["n_gpus"] == 1 and line["parity"]["mismatches"] == 0
     assert line["results_allgather"]["ranks_mismatched"] == 0
+    assert line["c5"]["parity"]["mismatches"] == 0
+
+
+def test_c5_full_size_one_gpu(gpu):
+    """SURVEY C5 at its full size on one GPU: 2^28 x 1472 B (395 GB) as 8
+    windows of 2^25 packets, each regenerated on the device with its own
+    seed.  Every packet is checked by the round-trip property -- word 0
+    zeroed, ip_cksum computed and stored there, wc_verify_strided must count
+    0 bad (the receiver's check, ip4.c:110-115) -- and window 0's checksums
+    are compared with the oracle, in 2^22-packet slices."""
+    import numpy as np
+    import torch
+
+    import warpcore_amd as wc
+    from oracle import c_oracle
+    from warpcore_amd import synth
+
+    L, win, windows = 1472, 1 << 25, 8
+    buf = torch.empty(win * L + 64, dtype=torch.uint8, device=gpu)
+    rows = buf[: win * L].view(win, L)
+    out = torch.empty(win, dtype=torch.uint16, device=gpu)
+    bad = torch.zeros(1, dtype=torch.int64, device=gpu)
+    for w in range(windows):
+        wc.synth_fill(buf, synth.SEED + 0xC5 * (w + 1), nbytes=win * L)
+        rows[:, 0:2] = 0
+        wc.cksum_strided(buf, L, L, win, out=out, kind="ip")
+        if w == 0:
+            sl = 1 << 22
+            for s0 in range(0, win, sl):
+                hb = buf[s0 * L:(s0 + sl) * L].cpu().numpy()
+                want = c_oracle.cksum_strided(hb, L, L, sl, kind=0)
+                got = out[s0:s0 + sl].cpu().numpy().view(np.uint16)
+                assert np.array_equal(got, want), f"window 0 slice {s0}"
+                del hb
+        rows[:, 0:2] = out.view(torch.uint8).view(win, 2)
+        _, b = wc.verify_strided(buf, L, L, win, kind="ip", out=out)
+        bad += b
+        torch.cuda.synchronize()
+        assert int(b.item()) == 0, f"window {w}: {int(b.item())} packets do not verify"
+    assert int(bad.item()) == 0
+    del rows, buf, out
+    torch.cuda.empty_cache()

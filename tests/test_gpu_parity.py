@@ -950,3 +950,30 @@ def test_fused_tx_then_rx_roundtrip(gpu, monkeypatch, mode):
     p_nonzero = p != 0          # a computed 0 is sent as "no checksum" (udp.c:212)
     assert (host(hdr2) == 0).all()
     assert (host(pay2)[p_nonzero] == 0).all()
+
+
+def test_production_lib_ignores_tuning_knobs(gpu, monkeypatch):
+    """WC_DIAG_NOLOAD=1 (no-load timing kernel) and WC_VARIANT=64 (no result
+    store) are tuning-build knobs: the shipped library must ignore them and
+    stay oracle-exact on C2 and C4."""
+    assert "TUNING" not in wc.version()
+    monkeypatch.setenv("WC_DIAG_NOLOAD", "1")
+    monkeypatch.setenv("WC_VARIANT", "64")
+    wc.reload_config()
+    n, L = 1 << 20, 1472
+    d = torch.empty(n * L + 64, dtype=torch.uint8, device=gpu)
+    wc.synth_fill(d, synth.SEED, nbytes=n * L)
+    out = torch.full((n,), 0xABCD, dtype=torch.int32, device=gpu).to(torch.int16).view(torch.uint16)
+    wc.cksum_strided(d, L, L, n, out=out)
+    np.testing.assert_array_equal(host(out), c_oracle.cksum_strided(d[:n * L].cpu().numpy(), L, L, n))
+    del d
+    lens = synth.zipf_lengths(1 << 24)
+    offs = synth.packed_offsets(lens)
+    total = int(offs[-1]) + int(lens[-1])
+    d = torch.empty(total + 64, dtype=torch.uint8, device=gpu)
+    wc.synth_fill(d, synth.SEED, nbytes=total)
+    for kind, k in (("ip", 0), ("payload", 1)):
+        got = wc.cksum_ragged(d, to_dev(offs, gpu), to_dev(lens, gpu), kind=kind)
+        np.testing.assert_array_equal(host(got), c_oracle.cksum_ragged(d[:total].cpu().numpy(),
+                                                                       offs, lens, kind=k))
+    del d

@@ -8,7 +8,8 @@ import numpy as np
 import pytest
 
 from oracle import c_oracle, py_oracle
-from packets import insert_checksum, ipv4_udp, ipv6_udp, pack, random_packets
+from packets import (RX_CASES, eth_frame, finish_udp, insert_checksum, ipv4_udp, ipv6_udp, pack,
+                     random_packets, rx_ring)
 
 GOLDEN = Path(__file__).resolve().parent / "golden"
 
@@ -143,3 +144,66 @@ def test_strided_matches_scalar():
     got = c_oracle.cksum_strided(buf, 1472, 1472, 64, threads=4)
     want = [c_oracle.ip_cksum(buf[i * 1472:(i + 1) * 1472]) for i in range(64)]
     np.testing.assert_array_equal(got, np.array(want, np.uint16))
+
+
+# ---------------------------------------------------------------------------
+# RX verdicts: the reference's RX checks (eth.c:77-87, ip4.c:95-138,
+# ip6.c:95-110, udp.c:99-139), two independent restatements.
+
+def test_rx_verdict_c_vs_py_every_case():
+    rng = np.random.default_rng(11)
+    frames = rx_ring(rng, 60 * len(RX_CASES), max_payload=700)
+    buf, offs, lens = pack(frames, align=1, lead=3)
+    got = c_oracle.rx_verdict_ragged(buf, offs, lens, threads=4)
+    b = buf.tobytes()
+    want = [py_oracle.rx_verdict(b[o:o + n], n) for o, n in zip(offs.tolist(), lens.tolist())]
+    np.testing.assert_array_equal(got, np.array(want, np.uint8))
+    # the frame mix reaches every verdict code
+    assert set(np.unique(got).tolist()) == set(range(10))
+
+
+def _v4_frame(rng, payload=b"x" * 100, **kw):
+    pkt, _ = ipv4_udp(payload, rng, **kw)
+    return eth_frame(finish_udp(pkt), rng)
+
+
+def test_rx_verdict_reference_details():
+    """Decisions where the reference is easy to misread."""
+    rng = np.random.default_rng(12)
+    v = py_oracle
+    f = _v4_frame(rng)
+    assert v.rx_verdict(f) == v.RX_OK and c_oracle.rx_verdict(f) == v.RX_OK
+    # More Fragments alone is not in IP4_OFFMASK 0xff1f (ip4.h:49): accepted
+    b = bytearray(f)
+    b[14 + 6] = 0x20
+    b[14 + 6:14 + 8] = b"\x20\x00"
+    fr = eth_frame(finish_udp(bytes(b[14:])), rng)
+    assert v.rx_verdict(fr) == v.RX_OK == c_oracle.rx_verdict(fr)
+    # a fragment offset (low 5 bits of byte 6 or byte 7) is dropped (ip4.c:122)
+    b = bytearray(f[14:])
+    b[7] = 1
+    fr = eth_frame(finish_udp(bytes(b)), rng)
+    assert v.rx_verdict(fr) == v.RX_FRAGMENT == c_oracle.rx_verdict(fr)
+    # a UDP checksum field of 0 skips the payload check (udp.c:132) even if
+    # the payload is corrupted afterwards
+    pkt, _ = ipv4_udp(b"y" * 50, rng)
+    fr = bytearray(eth_frame(finish_udp(pkt, zero_udp=True), rng))
+    fr[-1] ^= 0xFF
+    assert v.rx_verdict(bytes(fr)) == v.RX_OK_NO_CKSUM == c_oracle.rx_verdict(bytes(fr))
+    # IHL 0: ip_cksum(ip, 0) == 0xFFFF != 0 (ip4.c:111)
+    b = bytearray(f)
+    b[14] = 0x40
+    assert v.rx_verdict(bytes(b)) == v.RX_BAD_IP_CKSUM == c_oracle.rx_verdict(bytes(b))
+    # the frame ends inside the UDP payload: the reference would read past it
+    assert v.rx_verdict(f, len(f) - 1) == v.RX_TRUNCATED == c_oracle.rx_verdict(f, len(f) - 1)
+    # udp->len shorter than the datagram: only udp_len + hl is summed
+    # (udp.c:126, 134), so bytes after it do not matter
+    pkt, _ = ipv4_udp(b"z" * 64, rng)
+    b = bytearray(pkt)
+    b[20 + 4:20 + 6] = (8 + 10).to_bytes(2, "big")
+    fr = bytearray(eth_frame(finish_udp(bytes(b)), rng))
+    fr[14 + 20 + 8 + 30] ^= 0x55
+    assert v.rx_verdict(bytes(fr)) == v.RX_OK == c_oracle.rx_verdict(bytes(fr))
+    # ARP and the rest go to the host (eth.c:77-87)
+    arp = bytes(12) + b"\x08\x06" + bytes(28)
+    assert v.rx_verdict(arp) == v.RX_NOT_IP == c_oracle.rx_verdict(arp)

@@ -24,6 +24,12 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
 
+# WC_VARIANT / WC_DIAG_NOLOAD exist only in the tuning build (-DWC_TUNING,
+# libwccksum_tune.so): load it when a variant asks for them.
+if any(k in " ".join(sys.argv) for k in ("WC_VARIANT", "WC_DIAG_NOLOAD")) or \
+        any(k in os.environ for k in ("WC_VARIANT", "WC_DIAG_NOLOAD")):
+    os.environ.setdefault("WC_TUNING", "1")
+
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 

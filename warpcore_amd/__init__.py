@@ -10,7 +10,10 @@ from .cksum import (KIND_IP, KIND_PAYLOAD, WcError, cksum_host, cksum_host_multi
                     gpu_init_multi, shard_range,
                     cksum_ip_udp_strided, cksum_ragged, cksum_strided, gpu_init, host_register, host_unregister,
                     ip_cksum, payload_cksum, plan_strided, reload_config, synth_fill,
-                    verify_ragged, verify_strided, version)
+                    verify_ragged, verify_strided, version, shard_devices,
+                    rx_verdict_ragged, rx_verdict_host, RX_NAMES, RX_DROPS,
+                    RX_OK, RX_OK_NO_CKSUM, RX_BAD_IP_CKSUM, RX_BAD_UDP_CKSUM, RX_SHORT,
+                    RX_FRAGMENT, RX_BAD_VERSION, RX_NOT_UDP, RX_NOT_IP, RX_TRUNCATED)
 
 __all__ = [
     "KIND_IP", "KIND_PAYLOAD", "WcError", "cksum_host", "cksum_host_multi",
@@ -19,5 +22,7 @@ __all__ = [
     "cksum_ip_udp_strided", "cksum_ragged",
     "cksum_strided", "gpu_init", "host_register", "host_unregister", "ip_cksum",
     "payload_cksum", "plan_strided", "reload_config", "synth_fill", "verify_ragged",
-    "verify_strided", "version",
+    "verify_strided", "version", "shard_devices", "rx_verdict_ragged", "rx_verdict_host",
+    "RX_NAMES", "RX_DROPS", "RX_OK", "RX_OK_NO_CKSUM", "RX_BAD_IP_CKSUM", "RX_BAD_UDP_CKSUM",
+    "RX_SHORT", "RX_FRAGMENT", "RX_BAD_VERSION", "RX_NOT_UDP", "RX_NOT_IP", "RX_TRUNCATED",
 ]

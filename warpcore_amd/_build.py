@@ -3,9 +3,17 @@
 * ``libwccksum.so`` -- the product: gfx950 HIP kernels + C ABI
   (``include/warpcore_gpu/wc_cksum.h``), built in-tree with ``hipcc`` so the
   ``.so`` travels with the repo snapshot to the GPU box.
+* ``libwccksum_tune.so`` -- the same sources with ``-DWC_TUNING``: the
+  experimental kernel branches (``WC_VARIANT``) and the timing-only no-load
+  kernel (``WC_DIAG_NOLOAD``) are live there and nowhere else.  Only
+  ``tools/`` loads it (``WC_TUNING=1``); it is never the default.
 * ``oracle/libwc_oracle.so`` -- TEST INFRASTRUCTURE (parity checker / CPU
   baseline).  Built per host CPU model (``-march=native``), into
   ``oracle/build-<cpu>/`` so a box with a different host CPU rebuilds it.
+
+Staleness is decided by a hash of the sources and flags stored next to each
+library (``<lib>.srchash``), not by file times: a tree copied to another
+machine keeps its binary only if it was built from exactly these sources.
 """
 from __future__ import annotations
 
@@ -22,13 +30,18 @@ PKG = ROOT / "warpcore_amd"
 CSRC = PKG / "csrc"
 INCLUDE = ROOT / "include"
 LIB = PKG / "libwccksum.so"
+LIB_TUNE = PKG / "libwccksum_tune.so"
 ORACLE_DIR = ROOT / "oracle"
 
-HIP_SOURCES = [CSRC / "wc_k_strided.hip", CSRC / "wc_k_seg.hip", CSRC / "wc_k_flat.hip", CSRC / "wc_rccl.cpp",
-               CSRC / "wc_k_synth.hip", CSRC / "wc_cksum_api.cpp"]
-HIP_DEPS = HIP_SOURCES + [CSRC / "wc_cksum_kernels.h", CSRC / "wc_rccl.h", CSRC / "wc_device.h", CSRC / "wc_flat.h",
+HIP_SOURCES = [CSRC / "wc_k_strided.hip", CSRC / "wc_k_seg.hip", CSRC / "wc_k_flat.hip",
+               CSRC / "wc_k_rx.hip", CSRC / "wc_rccl.cpp", CSRC / "wc_k_synth.hip",
+               CSRC / "wc_cksum_api.cpp"]
+HIP_DEPS = HIP_SOURCES + [CSRC / "wc_cksum_kernels.h", CSRC / "wc_rccl.h", CSRC / "wc_device.h",
+                          CSRC / "wc_flat.h", CSRC / "wc_seg.h",
                           INCLUDE / "warpcore_gpu" / "wc_cksum.h"]
-ORACLE_SOURCES = [ORACLE_DIR / "wc_oracle.c", ORACLE_DIR / "wc_oracle.h"]
+ORACLE_SOURCES = [ORACLE_DIR / "wc_oracle.c", ORACLE_DIR / "wc_oracle.h", ORACLE_DIR / "Makefile"]
+BASE_FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall",
+              f"-I{INCLUDE}", f"-I{CSRC}"]
 
 
 def _hipcc() -> str:
@@ -38,20 +51,46 @@ def _hipcc() -> str:
     return "hipcc"
 
 
-def _stale(target: Path, deps) -> bool:
-    if not target.exists():
+def _src_hash(deps, flags) -> str:
+    h = hashlib.sha256()
+    for d in deps:
+        h.update(Path(d).name.encode())
+        h.update(Path(d).read_bytes())
+    h.update(" ".join(str(f) for f in flags).replace(str(ROOT), "<root>").encode())
+    return h.hexdigest()
+
+
+def _stamp(target: Path) -> Path:
+    return target.with_name(target.name + ".srchash")
+
+
+def _stale(target: Path, deps, flags) -> bool:
+    st = _stamp(target)
+    if not target.exists() or not st.exists():
         return True
-    t = target.stat().st_mtime
-    return any(Path(d).stat().st_mtime > t for d in deps)
+    return st.read_text().strip() != _src_hash(deps, flags)
 
 
-def build_lib(force: bool = False, verbose: bool = False) -> Path:
-    """Compile libwccksum.so for gfx950 (cross-compiles without a GPU): every
-    translation unit in parallel into a scratch directory, then one link."""
-    if not force and not _stale(LIB, HIP_DEPS):
-        return LIB
-    flags = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall",
-             f"-I{INCLUDE}", f"-I{CSRC}"]
+def lib_flags(tuning: bool = False) -> list:
+    return BASE_FLAGS + (["-DWC_TUNING"] if tuning else [])
+
+
+def lib_path(tuning: bool = False) -> Path:
+    return LIB_TUNE if tuning else LIB
+
+
+def lib_is_current(tuning: bool = False) -> bool:
+    return not _stale(lib_path(tuning), HIP_DEPS, lib_flags(tuning))
+
+
+def build_lib(force: bool = False, verbose: bool = False, tuning: bool = False) -> Path:
+    """Compile libwccksum.so (or the tuning build) for gfx950 -- cross-compiles
+    without a GPU: every translation unit in parallel into a scratch
+    directory, then one link."""
+    target, flags = lib_path(tuning), lib_flags(tuning)
+    if not force and not _stale(target, HIP_DEPS, flags):
+        return target
+    digest = _src_hash(HIP_DEPS, flags)
     with tempfile.TemporaryDirectory(prefix="wccksum-") as tmpdir:
         objs, procs = [], []
         for src in HIP_SOURCES:
@@ -64,13 +103,14 @@ def build_lib(force: bool = False, verbose: bool = False) -> Path:
         failed = [cmd for cmd, p in procs if p.wait() != 0]
         if failed:
             raise subprocess.CalledProcessError(1, failed[0])
-        tmp = LIB.with_suffix(".so.tmp")
+        tmp = target.with_suffix(".so.tmp")
         cmd = [_hipcc(), "--offload-arch=gfx950", "-fPIC", "-shared", "-o", str(tmp), *objs]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, target)
+    _stamp(target).write_text(digest + "\n")
+    return target
 
 
 def _cpu_tag() -> str:
@@ -92,7 +132,7 @@ def oracle_path() -> Path:
 def build_oracle(force: bool = False, verbose: bool = False) -> Path:
     """Compile the CPU restatement (test infrastructure) for this host CPU."""
     out = oracle_path()
-    if not force and not _stale(out, ORACLE_SOURCES):
+    if not force and not _stale(out, ORACLE_SOURCES, ["oracle"]):
         return out
     out.parent.mkdir(parents=True, exist_ok=True)
     tmp = out.with_suffix(".so.tmp")
@@ -101,13 +141,16 @@ def build_oracle(force: bool = False, verbose: bool = False) -> Path:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
     os.replace(tmp, out)
+    _stamp(out).write_text(_src_hash(ORACLE_SOURCES, ["oracle"]) + "\n")
     return out
 
 
-def build_all(force: bool = False, verbose: bool = False) -> None:
+def build_all(force: bool = False, verbose: bool = False, tuning: bool = False) -> None:
     build_lib(force=force, verbose=verbose)
+    if tuning:
+        build_lib(force=force, verbose=verbose, tuning=True)
     build_oracle(force=force, verbose=verbose)
 
 
 if __name__ == "__main__":
-    build_all(force="--force" in sys.argv, verbose=True)
+    build_all(force="--force" in sys.argv, verbose=True, tuning="--tuning" in sys.argv)

@@ -32,6 +32,8 @@ SIGNATURES = {
     "wc_verify_ragged": (_int, [_vp, _vp, _vp, _u64, _vp, _vp, _int, _vp]),
     "wc_cksum_ip_udp_strided": (_int, [_vp, _u64, _u16, _u64, _vp, _vp, _vp]),
     "wc_cksum_ip_udp_ragged": (_int, [_vp, _vp, _vp, _u64, _vp, _vp, _vp]),
+    "wc_rx_verdict_ragged": (_int, [_vp, _vp, _vp, _u64, _vp, _vp, _vp]),
+    "wc_rx_verdict_host": (_int, [_vp, _u64, _vp, _vp, _u64, _vp, _vp]),
     "wc_cksum_host": (_int, [_vp, _u64, _vp, _vp, _u64, _vp, _int]),
     "wc_host_register": (_int, [_vp, _u64]),
     "wc_host_unregister": (_int, [_vp]),
@@ -60,11 +62,14 @@ def load(build_if_missing: bool = True) -> ctypes.CDLL:
     with _lock:
         if _lib is not None:
             return _lib
-        path = _build.LIB
+        # WC_TUNING=1 (tools/ only): the -DWC_TUNING build, where the
+        # experimental WC_VARIANT branches and WC_DIAG_NOLOAD are live.
+        tuning = os.environ.get("WC_TUNING") == "1"
+        path = _build.lib_path(tuning)
         if os.environ.get("WC_LIB"):  # A/B tuning of two builds (tools/)
             path = _build.Path(os.environ["WC_LIB"])
         elif build_if_missing and os.environ.get("WC_NO_BUILD") != "1":
-            _build.build_lib()
+            _build.build_lib(tuning=tuning)
         if not path.exists():
             raise RuntimeError(
                 f"{path} is missing: the gfx950 HIP library must be built "

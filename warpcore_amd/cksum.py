@@ -272,14 +272,15 @@ def verify_ragged(base, offsets, lengths, kind="payload", out=None,
 
 
 def cksum_ip_udp_strided(base: torch.Tensor, stride: int, length: int, n: int,
-                         stream=None, byte_offset: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
+                         stream=None, byte_offset: int = 0, out_hdr: Optional[torch.Tensor] = None,
+                         out: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     """One pass over IP/UDP packets: (IPv4 header checksums, payload_cksum).
     The header checksum is ip_cksum(ip, ip4_hl) (ip4.c:110-115, 184-186); 0
     for IPv6 packets."""
     _same_device(base)
     _check_strided(base, byte_offset, stride, _check_len(length), n, KIND_PAYLOAD)
-    hdr = _out_tensor(None, n, base.device)
-    pay = _out_tensor(None, n, base.device)
+    hdr = _out_tensor(out_hdr, n, base.device)
+    pay = _out_tensor(out, n, base.device)
     with _on_device(base.device):
         _check("wc_cksum_ip_udp_strided", _lib.load().wc_cksum_ip_udp_strided(
             _dev_ptr(base) + byte_offset, stride, length, n, hdr.data_ptr(), pay.data_ptr(),
@@ -288,15 +289,79 @@ def cksum_ip_udp_strided(base: torch.Tensor, stride: int, length: int, n: int,
 
 
 def cksum_ip_udp_ragged(base: torch.Tensor, offsets: torch.Tensor, lengths: torch.Tensor,
-                        stream=None, check: bool = True) -> Tuple[torch.Tensor, torch.Tensor]:
+                        stream=None, check: bool = True, out_hdr: Optional[torch.Tensor] = None,
+                        out: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
     n = _check_ragged(base, offsets, lengths, KIND_PAYLOAD, check)
-    hdr = _out_tensor(None, n, base.device)
-    pay = _out_tensor(None, n, base.device)
+    hdr = _out_tensor(out_hdr, n, base.device)
+    pay = _out_tensor(out, n, base.device)
     with _on_device(base.device):
         _check("wc_cksum_ip_udp_ragged", _lib.load().wc_cksum_ip_udp_ragged(
             _dev_ptr(base), _dev_ptr(offsets), _dev_ptr(lengths), n, hdr.data_ptr(),
             pay.data_ptr(), _stream_ptr(stream, base.device)))
     return hdr, pay
+
+
+# --------------------------------------------------------------------------
+# RX verdicts (the reference's eth_rx -> ip4_rx / ip6_rx -> udp_rx checks).
+
+# enum wc_rx_verdict (include/warpcore_gpu/wc_cksum.h)
+RX_OK, RX_OK_NO_CKSUM, RX_BAD_IP_CKSUM, RX_BAD_UDP_CKSUM, RX_SHORT, RX_FRAGMENT, \
+    RX_BAD_VERSION, RX_NOT_UDP, RX_NOT_IP, RX_TRUNCATED = range(10)
+RX_NAMES = ("ok", "ok_no_cksum", "bad_ip_cksum", "bad_udp_cksum", "short", "fragment",
+            "bad_version", "not_udp", "not_ip", "truncated")
+RX_DROPS = (RX_BAD_IP_CKSUM, RX_BAD_UDP_CKSUM, RX_SHORT, RX_FRAGMENT, RX_BAD_VERSION,
+            RX_TRUNCATED)
+
+
+def rx_verdict_ragged(base: torch.Tensor, offsets: torch.Tensor, frame_lens: torch.Tensor,
+                      out: Optional[torch.Tensor] = None, stream=None,
+                      check: bool = True,
+                      drops: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """RX verdict of every Ethernet frame ``base[off[i] : off[i] + frame_len[i]]``
+    (a netmap RX ring's slot buffers and slot lengths): a uint8 code per frame
+    (``RX_*``) and the number of frames the reference's RX path drops.  No
+    header is parsed on the host (wc_rx_verdict_ragged).  A given ``drops``
+    tensor is accumulated into, not reset."""
+    _same_device(base, offsets=offsets, lengths=frame_lens)
+    n = _check_ragged_shapes(offsets, frame_lens)
+    if not base.is_contiguous():
+        raise ValueError("base must be contiguous")
+    if check and n:
+        _ragged_bounds(_nbytes(base), offsets, frame_lens, KIND_IP)
+    if out is None:
+        out = torch.empty(n, dtype=torch.uint8, device=base.device)
+    if out.numel() < n or out.element_size() != 1 or not out.is_contiguous() \
+            or out.device != base.device:
+        raise ValueError(f"out must be a contiguous 1-byte tensor of >= n entries on {base.device}")
+    if drops is None:
+        drops = torch.zeros(1, dtype=torch.int64, device=base.device)
+    elif drops.numel() < 1 or drops.element_size() != 8 or drops.device != base.device:
+        raise ValueError("drops must be an 8-byte device tensor (accumulated)")
+    with _on_device(base.device):
+        _check("wc_rx_verdict_ragged", _lib.load().wc_rx_verdict_ragged(
+            _dev_ptr(base), _dev_ptr(offsets), _dev_ptr(frame_lens), n, out.data_ptr(),
+            drops.data_ptr(), _stream_ptr(stream, base.device)))
+    return out, drops
+
+
+def rx_verdict_host(buf: np.ndarray, offsets: np.ndarray,
+                    frame_lens: np.ndarray) -> Tuple[np.ndarray, int]:
+    """rx_verdict_ragged over host memory (wc_rx_verdict_host, synchronous):
+    (uint8 verdicts, drop count)."""
+    buf = np.ascontiguousarray(buf).reshape(-1).view(np.uint8)
+    lens_in = np.asarray(frame_lens)
+    if lens_in.size and (lens_in.min() < 0 or lens_in.max() > 0xFFFF):
+        raise ValueError("frame lengths are uint16 (netmap_slot.len)")
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    lens = np.ascontiguousarray(lens_in, dtype=np.uint16)
+    if off.shape != lens.shape:
+        raise ValueError("offsets and frame_lens must have the same shape")
+    out = np.empty(off.size, dtype=np.uint8)
+    drops = ctypes.c_uint64()
+    _check("wc_rx_verdict_host", _lib.load().wc_rx_verdict_host(
+        buf.ctypes.data, buf.size, off.ctypes.data, lens.ctypes.data, off.size,
+        out.ctypes.data, ctypes.byref(drops)))
+    return out, int(drops.value)
 
 
 # --------------------------------------------------------------------------
@@ -376,15 +441,29 @@ def shard_range(n: int, g: int, ngpus: int) -> Tuple[int, int]:
     return lo.value, hi.value
 
 
+_shard_devices: list = []
+
+
 def gpu_init_multi(ngpus: int = 0, devices=None) -> int:
     """Set up one shard executor per device (devices[g], or g); returns G."""
+    global _shard_devices
     arr = None
     if devices is not None:
-        devices = list(devices)
+        devices = [int(d) for d in devices]
         ngpus = len(devices)
         arr = (ctypes.c_int * ngpus)(*devices)
     _check("wc_gpu_init_multi", _lib.load().wc_gpu_init_multi(ngpus, arr))
-    return int(_lib.load().wc_gpu_multi_count())
+    G = int(_lib.load().wc_gpu_multi_count())
+    _shard_devices = list(devices) if devices is not None else list(range(G))
+    return G
+
+
+def shard_devices() -> list:
+    """Device index of every shard executor (after gpu_init_multi)."""
+    G = int(_lib.load().wc_gpu_multi_count())
+    if len(_shard_devices) != G:
+        raise RuntimeError("shard executors not set up by gpu_init_multi")
+    return list(_shard_devices)
 
 
 def cksum_host_multi(buf: np.ndarray, offsets: np.ndarray, lengths: np.ndarray,
@@ -410,28 +489,64 @@ def _ptrs(ts) -> ctypes.Array:
                                          for t in ts])
 
 
+def _per_shard(name: str, items, devs) -> list:
+    """The C side reads one entry per shard executor from every array: each
+    list must have exactly that many entries, each on its shard's device."""
+    items = list(items)
+    if len(items) != len(devs):
+        raise ValueError(f"{name}: {len(items)} entries for {len(devs)} shard executors")
+    for g, (t, d) in enumerate(zip(items, devs)):
+        if t is None:
+            continue
+        if not isinstance(t, torch.Tensor) or not t.is_cuda:
+            raise ValueError(f"{name}[{g}] must be a device (cuda) tensor")
+        if t.device.index != d:
+            raise ValueError(f"{name}[{g}] is on {t.device}, shard {g} runs on cuda:{d}")
+    return items
+
+
+def _shard_streams(streams, devs):
+    if streams is None:
+        return _ptrs([_stream_ptr(None, torch.device("cuda", d)) for d in devs])
+    streams = list(streams)
+    if len(streams) != len(devs):
+        raise ValueError(f"streams: {len(streams)} entries for {len(devs)} shard executors")
+    return _ptrs([_stream_ptr(s, torch.device("cuda", d)) for s, d in zip(streams, devs)])
+
+
 def cksum_ragged_multi(bases, offsets, lengths, outs, kind="ip", streams=None) -> None:
     """Shard g's device-resident batch (bases[g], offsets[g], lengths[g]) into
     outs[g], each on shard g's device (asynchronous)."""
     k = _kind(kind)
-    G = len(bases)
+    devs = shard_devices()
+    bases = _per_shard("bases", bases, devs)
+    offsets = _per_shard("offsets", offsets, devs)
+    lengths = _per_shard("lengths", lengths, devs)
+    outs = _per_shard("outs", outs, devs)
     for b, o, l, r in zip(bases, offsets, lengths, outs):
         n = _check_ragged(b, o, l, k, True)
         _out_tensor(r, n, b.device)
-    ns = (ctypes.c_uint64 * G)(*[o.numel() for o in offsets])
-    st = None if streams is None else _ptrs([_stream_ptr(s) for s in streams])
+    ns = (ctypes.c_uint64 * len(devs))(*[o.numel() for o in offsets])
     _check("wc_cksum_ragged_multi", _lib.load().wc_cksum_ragged_multi(
-        _ptrs(bases), _ptrs(offsets), _ptrs(lengths), ns, _ptrs(outs), k, st))
+        _ptrs(bases), _ptrs(offsets), _ptrs(lengths), ns, _ptrs(outs), k,
+        _shard_streams(streams, devs)))
 
 
 def gather_results_multi(shard_outs, counts, all_outs, streams=None) -> None:
     """RCCL all-gather of every shard's results into all_outs[g] (packet order)."""
-    G = len(shard_outs)
-    total = sum(int(c) for c in counts)
-    for a in all_outs:
-        if a.numel() < total or a.element_size() != 2:
-            raise ValueError("each all_outs tensor needs sum(counts) 2-byte entries")
-    ns = (ctypes.c_uint64 * G)(*[int(c) for c in counts])
-    st = None if streams is None else _ptrs([_stream_ptr(s) for s in streams])
+    devs = shard_devices()
+    shard_outs = _per_shard("shard_outs", shard_outs, devs)
+    all_outs = _per_shard("all_outs", all_outs, devs)
+    counts = [int(c) for c in counts]
+    if len(counts) != len(devs):
+        raise ValueError(f"counts: {len(counts)} entries for {len(devs)} shard executors")
+    total = sum(counts)
+    for g, (src, c) in enumerate(zip(shard_outs, counts)):
+        if c < 0 or src.numel() < c or src.element_size() != 2 or not src.is_contiguous():
+            raise ValueError(f"shard_outs[{g}] needs >= {c} contiguous 2-byte entries")
+    for g, a in enumerate(all_outs):
+        if a.numel() < total or a.element_size() != 2 or not a.is_contiguous():
+            raise ValueError("each all_outs tensor needs sum(counts) contiguous 2-byte entries")
+    ns = (ctypes.c_uint64 * len(devs))(*counts)
     _check("wc_gather_results_multi", _lib.load().wc_gather_results_multi(
-        _ptrs(shard_outs), ns, _ptrs(all_outs), st))
+        _ptrs(shard_outs), ns, _ptrs(all_outs), _shard_streams(streams, devs)))

@@ -32,6 +32,9 @@ constexpr uint64_t kChunkPkts = 1ull << 20;       // host-path packets per chunk
 constexpr uint64_t kScalarStage = 65536 + 64;     // one max-size packet
 constexpr uint64_t kZcPkts = 4096;                // zero-copy path: max packets
 constexpr int kFlatMinDefault = 0;                // ragged: flat kernel from n >= this
+// Internal batch kind of the host paths beside WC_CKSUM_IP / WC_CKSUM_PAYLOAD:
+// RX verdicts of Ethernet frames (lengths = frame lengths, 1-byte results).
+constexpr int kKindRx = 2;
 
 // Small batches over registered memory skip the copy engines: the kernel
 // reads the packets straight out of the page-locked region over PCIe, and
@@ -79,7 +82,9 @@ struct Device {
 
 struct Registration {
     uint64_t bytes;
-    const uint8_t *dptr; // device address of the region's first byte
+    // Device address of the region's first byte, looked up per device on
+    // first use (hipHostGetDevicePointer with that device current).
+    const uint8_t *dptr[kMaxDevices] = {};
 };
 
 // Tuning knobs (the WC_* environment), read once when the library first
@@ -89,7 +94,7 @@ struct Registration {
 struct Config {
     int blocks_per_cu = 0;         // WC_BLOCKS_PER_CU: cap the one-shot grid
     int grid = 0;                  // WC_GRID: fixed grid (grid-stride)
-    int variant = 0;               // WC_VARIANT: experimental kernel variants
+    int variant = 0;               // WC_VARIANT: experimental kernel variants (tuning build)
     bool have_shape = false;       // WC_SHAPE=G,CPL,U: force the strided shape
     wc::Shape shape{};
     bool have_rshape = false;      // WC_RAGGED_SHAPE: small ragged group shape
@@ -104,7 +109,7 @@ struct Config {
     int zc_group_max = (int)kZcGroupMax; // WC_ZC_GROUP_MAX
     int zc_bytes = kZcBytesDefault;      // WC_ZC_BYTES
     uint64_t flat_min = kFlatMinDefault; // WC_FLAT_MIN: ragged group kernel below this n
-    int diag_noload = 0;           // WC_DIAG_NOLOAD: timing-only build
+    int diag_noload = 0;           // WC_DIAG_NOLOAD: timing-only kernel (tuning build)
     int nt = 1;                    // WC_NT: nontemporal loads
     int grp_dense = 65;            // WC_GRP_DENSE (64ths; 65 = never)
     int grp_sparse = 40;           // WC_GRP_SPARSE
@@ -154,9 +159,19 @@ bool parse_shape(const char *v, wc::Shape *sh)
 void load_config_locked()
 {
     Config c;
+    // Every knob below only chooses among exact paths (shapes, grids, tile
+    // paths, load flavour): results stay bit-identical whatever they say.
+    // The two that do not -- WC_VARIANT (experimental kernel branches, one of
+    // which drops the result store) and WC_DIAG_NOLOAD (a timing-only build
+    // that reads no packet bytes) -- exist only in the tuning build
+    // (-DWC_TUNING, libwccksum_tune.so for tools/); the shipped library
+    // ignores them.
     c.blocks_per_cu = env_int("WC_BLOCKS_PER_CU", c.blocks_per_cu);
     c.grid = env_int("WC_GRID", c.grid);
+#ifdef WC_TUNING
     c.variant = env_int("WC_VARIANT", c.variant);
+    c.diag_noload = env_int("WC_DIAG_NOLOAD", c.diag_noload);
+#endif
     c.have_shape = parse_shape(getenv("WC_SHAPE"), &c.shape);
     c.have_rshape = parse_shape(getenv("WC_RAGGED_SHAPE"), &c.rshape);
     c.strided_seg = env_int("WC_STRIDED_SEG", c.strided_seg);
@@ -169,7 +184,6 @@ void load_config_locked()
     c.zc_group_max = env_int("WC_ZC_GROUP_MAX", c.zc_group_max);
     c.zc_bytes = env_int("WC_ZC_BYTES", c.zc_bytes);
     c.flat_min = env_u64("WC_FLAT_MIN", c.flat_min);
-    c.diag_noload = env_int("WC_DIAG_NOLOAD", c.diag_noload);
     c.nt = env_int("WC_NT", c.nt);
     c.grp_dense = env_int("WC_GRP_DENSE", c.grp_dense);
     c.grp_sparse = env_int("WC_GRP_SPARSE", c.grp_sparse);
@@ -521,37 +535,12 @@ uint16_t scalar_cksum(const void *buf, uint16_t len, int kind, const char *who)
 // ---------------------------------------------------------------------------
 // Host-memory pipeline.
 
-// Streams, events and staging of one host pipeline, created on the current
-// device.
-int pipe_init_locked(HostPipe &P)
-{
-    if (P.ready)
-        return WC_OK;
-    for (int s = 0; s < kPipe; ++s) {
-        if (hipStreamCreateWithFlags(&P.st[s], hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&P.done[s], hipEventDisableTiming) != hipSuccess)
-            return WC_ENOMEM;
-        if (hipMalloc((void **)&P.d_bytes[s], kChunkBytes + 64) != hipSuccess ||
-            hipMalloc((void **)&P.d_off[s], kChunkPkts * 8) != hipSuccess ||
-            hipMalloc((void **)&P.d_len[s], kChunkPkts * 2) != hipSuccess ||
-            hipMalloc((void **)&P.d_out[s], kChunkPkts * 2) != hipSuccess)
-            return WC_ENOMEM;
-        if (hipHostMalloc((void **)&P.h_bytes[s], kChunkBytes + 64, 0) != hipSuccess ||
-            hipHostMalloc((void **)&P.h_off[s], kChunkPkts * 8, 0) != hipSuccess ||
-            hipHostMalloc((void **)&P.h_len[s], kChunkPkts * 2, 0) != hipSuccess ||
-            hipHostMalloc((void **)&P.h_out[s], kChunkPkts * 2, 0) != hipSuccess)
-            return WC_ENOMEM;
-    }
-    P.ready = true;
-    return WC_OK;
-}
-
+// Frees whatever a (possibly partly built) pipeline holds.
 void pipe_free(HostPipe &P)
 {
-    if (!P.ready)
-        return;
     for (int s = 0; s < kPipe; ++s) {
-        (void)hipStreamSynchronize(P.st[s]);
+        if (P.st[s])
+            (void)hipStreamSynchronize(P.st[s]);
         (void)hipFree(P.d_bytes[s]);
         (void)hipFree(P.d_off[s]);
         (void)hipFree(P.d_len[s]);
@@ -560,10 +549,37 @@ void pipe_free(HostPipe &P)
         (void)hipHostFree(P.h_off[s]);
         (void)hipHostFree(P.h_len[s]);
         (void)hipHostFree(P.h_out[s]);
-        (void)hipEventDestroy(P.done[s]);
-        (void)hipStreamDestroy(P.st[s]);
+        if (P.done[s])
+            (void)hipEventDestroy(P.done[s]);
+        if (P.st[s])
+            (void)hipStreamDestroy(P.st[s]);
     }
     P = HostPipe{};
+}
+
+// Streams, events and staging of one host pipeline, created on the current
+// device.
+int pipe_init_locked(HostPipe &P)
+{
+    if (P.ready)
+        return WC_OK;
+    for (int s = 0; s < kPipe; ++s) {
+        if (hipStreamCreateWithFlags(&P.st[s], hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&P.done[s], hipEventDisableTiming) != hipSuccess ||
+            hipMalloc((void **)&P.d_bytes[s], kChunkBytes + 64) != hipSuccess ||
+            hipMalloc((void **)&P.d_off[s], kChunkPkts * 8) != hipSuccess ||
+            hipMalloc((void **)&P.d_len[s], kChunkPkts * 2) != hipSuccess ||
+            hipMalloc((void **)&P.d_out[s], kChunkPkts * 2) != hipSuccess ||
+            hipHostMalloc((void **)&P.h_bytes[s], kChunkBytes + 64, 0) != hipSuccess ||
+            hipHostMalloc((void **)&P.h_off[s], kChunkPkts * 8, 0) != hipSuccess ||
+            hipHostMalloc((void **)&P.h_len[s], kChunkPkts * 2, 0) != hipSuccess ||
+            hipHostMalloc((void **)&P.h_out[s], kChunkPkts * 2, 0) != hipSuccess) {
+            pipe_free(P);
+            return WC_ENOMEM;
+        }
+    }
+    P.ready = true;
+    return WC_OK;
 }
 
 int zc_init_locked(Device &D)
@@ -584,8 +600,11 @@ int zc_init_locked(Device &D)
     return WC_OK;
 }
 
-// Device address of host range [p, p + bytes) if it lies inside one
-// registered region, else nullptr.
+// Address on the CURRENT device of host range [p, p + bytes) if it lies
+// inside one registered region, else nullptr.  The region was registered
+// portable and mapped; its device address is looked up for this device the
+// first time (a batch may run on a shard device other than the one current
+// at wc_host_register).
 const uint8_t *registered_dptr_locked(const void *p, uint64_t bytes)
 {
     const uintptr_t a = (uintptr_t)p;
@@ -595,7 +614,17 @@ const uint8_t *registered_dptr_locked(const void *p, uint64_t bytes)
     --it;
     if (a < it->first || a + bytes > it->first + it->second.bytes)
         return nullptr;
-    return it->second.dptr + (a - it->first);
+    int dev = 0;
+    if (current_device(&dev) != WC_OK)
+        return nullptr;
+    const uint8_t *&d = it->second.dptr[dev];
+    if (!d) {
+        void *dp = nullptr;
+        if (hipHostGetDevicePointer(&dp, (void *)it->first, 0) != hipSuccess)
+            return nullptr;
+        d = (const uint8_t *)dp;
+    }
+    return d + (a - it->first);
 }
 
 // Bytes the reference reads for one packet (payload_cksum reads the IPv4
@@ -605,9 +634,28 @@ uint64_t span_of(uint16_t len, int kind)
     return kind == WC_CKSUM_PAYLOAD ? std::max<uint64_t>(len, 20) : len;
 }
 
+// Result bytes per packet: a uint16 checksum, or a uint8 RX verdict.
+int out_size(int kind) { return kind == kKindRx ? 1 : 2; }
+
+// One device launch over a ragged batch of `kind` (a checksum kind or RX
+// verdicts; lengths are frame lengths for the latter).
+int run_ragged_any(const Device &D, const Config &C, const uint8_t *d_base, const uint64_t *d_off,
+                   const uint16_t *d_len, uint64_t n, void *d_out, int kind, bool zero_copy,
+                   hipStream_t st)
+{
+    if (kind == kKindRx)
+        return hip_err(wc::launch_rx_verdict(d_base, d_off, d_len, n, (uint8_t *)d_out, nullptr,
+                                             C.nt != 0, st));
+    const Plan p = plan_ragged(D, C, n, kind, zero_copy);
+    wc::LaunchArgs a{d_base, 0,       0,    d_off, d_len, n,
+                     (uint16_t *)d_out, nullptr, kind, true,  false, C.nt != 0,
+                     C.flat_tpw};
+    return run(D, C, a, p, st);
+}
+
 // Small registered batch: one launch reading host memory in place.
 int host_zero_copy(Device &D, const uint8_t *dbase, const uint64_t *h_off,
-                   const uint16_t *h_len, uint64_t n, uint16_t *h_out, int kind)
+                   const uint16_t *h_len, uint64_t n, uint8_t *h_out, int kind)
 {
     int rc = zc_init_locked(D);
     if (rc)
@@ -615,18 +663,13 @@ int host_zero_copy(Device &D, const uint8_t *dbase, const uint64_t *h_off,
     ZeroCopy &Z = D.zc;
     memcpy(Z.h_off, h_off, n * 8);
     memcpy(Z.h_len, h_len, n * 2);
-    const Config &C = g_cfg;
-    const Plan p = plan_ragged(D, C, n, kind, true);
-    wc::LaunchArgs a{dbase, 0,       0,    Z.d_off, Z.d_len, n,
-                     Z.d_out, nullptr, kind, true,    false,   C.nt != 0,
-                     C.flat_tpw};
-    rc = run(D, C, a, p, Z.st);
+    rc = run_ragged_any(D, g_cfg, dbase, Z.d_off, Z.d_len, n, Z.d_out, kind, true, Z.st);
     if (rc)
         return rc;
     hipError_t e = hipStreamSynchronize(Z.st);
     if (e != hipSuccess)
         return hip_err(e);
-    memcpy(h_out, (const void *)Z.h_out, n * 2);
+    memcpy(h_out, (const void *)Z.h_out, n * out_size(kind));
     return WC_OK;
 }
 
@@ -647,7 +690,7 @@ struct PipeRun {
     bool registered = false, ascending = true;
     const uint64_t *h_off = nullptr;
     const uint16_t *h_len = nullptr;
-    uint16_t *h_out = nullptr;
+    uint8_t *h_out = nullptr; // out_size(kind) bytes per packet
     int kind = WC_CKSUM_IP;
     uint64_t i = 0, hi = 0;
     uint64_t pend_lo[kPipe] = {}, pend_n[kPipe] = {};
@@ -664,7 +707,8 @@ struct PipeRun {
         hipError_t e = hipEventSynchronize(P->done[s]);
         if (e != hipSuccess)
             return hip_err(e);
-        memcpy(h_out + pend_lo[s], P->h_out[s], pend_n[s] * 2);
+        const int osz = out_size(kind);
+        memcpy(h_out + pend_lo[s] * osz, P->h_out[s], pend_n[s] * osz);
         pend[s] = false;
         return WC_OK;
     }
@@ -732,15 +776,12 @@ struct PipeRun {
                                st);
         if (e != hipSuccess)
             return hip_err(e);
-        const Config &C = g_cfg;
-        const Plan p = plan_ragged(*D, C, cnt, kind);
-        wc::LaunchArgs a{P->d_bytes[slot], 0,    0,    P->d_off[slot], P->d_len[slot],
-                         cnt,              P->d_out[slot], nullptr, kind, true,
-                         false,            C.nt != 0,      C.flat_tpw};
-        rc = run(*D, C, a, p, st);
+        rc = run_ragged_any(*D, g_cfg, P->d_bytes[slot], P->d_off[slot], P->d_len[slot], cnt,
+                            P->d_out[slot], kind, false, st);
         if (rc)
             return rc;
-        e = hipMemcpyAsync(P->h_out[slot], P->d_out[slot], cnt * 2, hipMemcpyDeviceToHost, st);
+        e = hipMemcpyAsync(P->h_out[slot], P->d_out[slot], cnt * out_size(kind),
+                           hipMemcpyDeviceToHost, st);
         if (e == hipSuccess)
             e = hipEventRecord(P->done[slot], st);
         if (e != hipSuccess)
@@ -792,7 +833,7 @@ void shard_range(uint64_t n, int g, int G, uint64_t *lo, uint64_t *hi)
 
 int host_pipeline(Device &D, const uint8_t *hb, bool registered, bool ascending,
                   const uint64_t *h_off, const uint16_t *h_len, uint64_t n,
-                  uint16_t *h_out, int kind)
+                  uint8_t *h_out, int kind)
 {
     PipeRun r;
     r.D = &D;
@@ -842,6 +883,35 @@ int for_each_shard(F &&fn)
     }
     (void)hipSetDevice(cur);
     return rc;
+}
+
+// wc_cksum_host / wc_rx_verdict_host: a host-memory batch on the current
+// device -- zero-copy for a small registered batch, else the pipeline.
+int host_batch(const void *h_base, uint64_t h_bytes, const uint64_t *h_off,
+               const uint16_t *h_len, uint64_t n, uint8_t *h_out, int kind)
+{
+    if (n == 0)
+        return WC_OK;
+    if (!h_base || !h_off || !h_len || !h_out)
+        return WC_EINVAL;
+    bool ascending = true;
+    uint64_t total = 0;
+    if (!host_batch_ok(h_bytes, h_off, h_len, n, kind, &ascending, &total))
+        return WC_EINVAL;
+
+    std::lock_guard<std::mutex> lk(g_mu);
+    Device *D = nullptr;
+    int rc = init_locked(-1, &D);
+    if (rc)
+        return rc;
+    const uint8_t *dbase = registered_dptr_locked(h_base, h_bytes);
+    if (dbase && n <= kZcPkts && total <= (uint64_t)g_cfg.zc_bytes)
+        return host_zero_copy(*D, dbase, h_off, h_len, n, h_out, kind);
+    rc = pipe_init_locked(D->pipe);
+    if (rc)
+        return rc;
+    return host_pipeline(*D, (const uint8_t *)h_base, dbase != nullptr, ascending,
+                         h_off, h_len, n, h_out, kind);
 }
 
 } // namespace
@@ -925,6 +995,15 @@ int wc_host_register(void *h_ptr, uint64_t bytes)
     int rc = init_locked(-1, &D);
     if (rc)
         return rc;
+    // Registering a region again is a no-op (it stays registered across
+    // wc_gpu_fini); a larger size re-registers it.
+    auto it = g_registered.find((uintptr_t)h_ptr);
+    if (it != g_registered.end()) {
+        if (it->second.bytes >= bytes)
+            return WC_OK;
+        g_registered.erase(it);
+        (void)hipHostUnregister(h_ptr);
+    }
     // Portable: every device (wc_cksum_host_multi's shards) may DMA from it.
     hipError_t e = hipHostRegister(h_ptr, bytes, hipHostRegisterMapped | hipHostRegisterPortable);
     if (e != hipSuccess)
@@ -935,7 +1014,12 @@ int wc_host_register(void *h_ptr, uint64_t bytes)
         (void)hipHostUnregister(h_ptr);
         return hip_err(e);
     }
-    g_registered[(uintptr_t)h_ptr] = Registration{bytes, (const uint8_t *)dptr};
+    Registration reg;
+    reg.bytes = bytes;
+    int dev = 0;
+    if (current_device(&dev) == WC_OK)
+        reg.dptr[dev] = (const uint8_t *)dptr;
+    g_registered[(uintptr_t)h_ptr] = reg;
     return WC_OK;
 }
 
@@ -956,28 +1040,39 @@ int wc_cksum_host(const void *h_base, uint64_t h_bytes, const uint64_t *h_off,
 {
     if (kind != WC_CKSUM_IP && kind != WC_CKSUM_PAYLOAD)
         return WC_EINVAL;
+    return host_batch(h_base, h_bytes, h_off, h_len, n, (uint8_t *)h_out, kind);
+}
+
+int wc_rx_verdict_ragged(const void *d_base, const uint64_t *d_off, const uint16_t *d_frame_len,
+                         uint64_t n, uint8_t *d_verdict, uint64_t *d_drops, void *stream)
+{
     if (n == 0)
         return WC_OK;
-    if (!h_base || !h_off || !h_len || !h_out)
+    if (!d_base || !d_off || !d_frame_len || !d_verdict)
         return WC_EINVAL;
-    bool ascending = true;
-    uint64_t total = 0;
-    if (!host_batch_ok(h_bytes, h_off, h_len, n, kind, &ascending, &total))
-        return WC_EINVAL;
-
-    std::lock_guard<std::mutex> lk(g_mu);
     Device *D = nullptr;
-    int rc = init_locked(-1, &D);
+    Config C;
+    int rc = ensure_device(&D, &C);
     if (rc)
         return rc;
-    const uint8_t *dbase = registered_dptr_locked(h_base, h_bytes);
-    if (dbase && n <= kZcPkts && total <= (uint64_t)g_cfg.zc_bytes)
-        return host_zero_copy(*D, dbase, h_off, h_len, n, h_out, kind);
-    rc = pipe_init_locked(D->pipe);
-    if (rc)
-        return rc;
-    return host_pipeline(*D, (const uint8_t *)h_base, dbase != nullptr, ascending,
-                         h_off, h_len, n, h_out, kind);
+    return hip_err(wc::launch_rx_verdict(d_base, d_off, d_frame_len, n, d_verdict, d_drops,
+                                         C.nt != 0, (hipStream_t)stream));
+}
+
+int wc_rx_verdict_host(const void *h_base, uint64_t h_bytes, const uint64_t *h_off,
+                       const uint16_t *h_frame_len, uint64_t n, uint8_t *h_verdict,
+                       uint64_t *h_drops)
+{
+    if (n && !h_verdict)
+        return WC_EINVAL;
+    const int rc = host_batch(h_base, h_bytes, h_off, h_frame_len, n, h_verdict, kKindRx);
+    if (rc == WC_OK && h_drops) {
+        uint64_t d = 0;
+        for (uint64_t i = 0; i < n; ++i)
+            d += WC_RX_IS_DROP(h_verdict[i]);
+        *h_drops = d;
+    }
+    return rc;
 }
 
 // ---------------------------------------------------------------------------
@@ -1023,14 +1118,28 @@ int wc_gpu_init_multi(int ngpus, const int *devices)
         g_shard[g] = ShardExec{};
     }
     g_multi_n = 0;
+    // All or nothing: a shard that fails to come up (its device's scratch or
+    // its pipeline) tears down the ones built before it, so a later
+    // wc_cksum_host_multi never runs on a half-built executor -- it falls
+    // back to the current device, as before any wc_gpu_init_multi.
     int rc = WC_OK;
+    int built = 0;
     for (int g = 0; g < ngpus && rc == WC_OK; ++g) {
         Device *D = nullptr;
         rc = init_locked(devs[g], &D); // sets device devs[g]
+        g_shard[g].dev = devs[g];
         if (rc == WC_OK)
             rc = pipe_init_locked(g_shard[g].pipe);
-        g_shard[g].dev = devs[g];
-        g_multi_n = g + 1;
+        built = g + 1; // pipe_free below also frees a partly built pipe
+    }
+    if (rc != WC_OK) {
+        for (int g = 0; g < built; ++g) {
+            (void)hipSetDevice(g_shard[g].dev);
+            pipe_free(g_shard[g].pipe);
+            g_shard[g] = ShardExec{};
+        }
+    } else {
+        g_multi_n = ngpus;
     }
     (void)hipSetDevice(cur);
     return rc;
@@ -1068,13 +1177,17 @@ int wc_cksum_host_multi(const void *h_base, uint64_t h_bytes, const uint64_t *h_
         int cur = 0;
         if (hipGetDevice(&cur) != hipSuccess)
             return WC_ENODEV;
-        const uint8_t *dbase = registered_dptr_locked(h_base, h_bytes);
-        if (dbase && n <= kZcPkts && total <= (uint64_t)g_cfg.zc_bytes) {
-            // Small registered batch: one zero-copy launch on shard 0.
+        const bool registered = registered_dptr_locked(h_base, h_bytes) != nullptr;
+        if (registered && n <= kZcPkts && total <= (uint64_t)g_cfg.zc_bytes) {
+            // Small registered batch: one zero-copy launch on shard 0, with
+            // the region's address as shard 0's device sees it.
             Device *D = nullptr;
-            int rc = init_locked(g_shard[0].dev, &D);
+            int rc = init_locked(g_shard[0].dev, &D); // sets shard 0's device
+            const uint8_t *dbase = rc == WC_OK ? registered_dptr_locked(h_base, h_bytes) : nullptr;
+            if (rc == WC_OK && !dbase)
+                rc = WC_EINVAL;
             if (rc == WC_OK)
-                rc = host_zero_copy(*D, dbase, h_off, h_len, n, h_out, kind);
+                rc = host_zero_copy(*D, dbase, h_off, h_len, n, (uint8_t *)h_out, kind);
             (void)hipSetDevice(cur);
             return rc;
         }
@@ -1085,11 +1198,11 @@ int wc_cksum_host_multi(const void *h_base, uint64_t h_bytes, const uint64_t *h_
             r.P = &g_shard[g].pipe;
             r.dev = g_shard[g].dev;
             r.hb = (const uint8_t *)h_base;
-            r.registered = dbase != nullptr;
+            r.registered = registered;
             r.ascending = ascending;
             r.h_off = h_off;
             r.h_len = h_len;
-            r.h_out = h_out;
+            r.h_out = (uint8_t *)h_out;
             r.kind = kind;
             shard_range(n, g, G, &r.i, &r.hi);
         }
@@ -1204,12 +1317,10 @@ int wc_gpu_fini(void)
         (void)hipHostFree(D.h_res);
         D = Device{};
     }
-    // Drop the library's page-locks too: a later wc_gpu_init starts clean
-    // (a region still wanted must be registered again), and it re-reads the
-    // WC_* configuration.
-    for (auto &r : g_registered)
-        (void)hipHostUnregister((void *)r.first);
-    g_registered.clear();
+    // Page-locks taken with wc_host_register belong to the caller and stay
+    // until wc_host_unregister (a ring registered once keeps its zero-copy
+    // path across fini / init).  The WC_* configuration is re-read at the
+    // next initialisation.
     g_cfg_loaded = false;
     if (have_cur)
         (void)hipSetDevice(cur);
@@ -1283,6 +1394,10 @@ const char *wc_strerror(int err)
     }
 }
 
-const char *wc_version(void) { return "wccksum 0.1.0 (gfx950)"; }
+#ifdef WC_TUNING
+const char *wc_version(void) { return "wccksum 0.3.0 (gfx950, TUNING build: WC_VARIANT/WC_DIAG_NOLOAD live)"; }
+#else
+const char *wc_version(void) { return "wccksum 0.3.0 (gfx950)"; }
+#endif
 
 } // extern "C"

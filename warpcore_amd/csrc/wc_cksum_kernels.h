@@ -125,5 +125,10 @@ hipError_t launch_flat(const LaunchArgs &a, int rows, hipStream_t st);
 hipError_t launch_flat_kernel(const LaunchArgs &a, int rows, hipStream_t st);
 hipError_t launch_synth(void *buf, uint64_t nbytes, uint64_t seed, int grid,
                         hipStream_t st);
+// RX verdicts of Ethernet frames [base + offs[i], + flens[i]) (wc_k_rx.hip);
+// drops (optional) accumulates the frames the reference's RX path drops.
+hipError_t launch_rx_verdict(const void *base, const uint64_t *offs, const uint16_t *flens,
+                             uint64_t n, uint8_t *verdict, uint64_t *drops, bool nt,
+                             hipStream_t st);
 
 } // namespace wc

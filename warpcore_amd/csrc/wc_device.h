@@ -70,6 +70,20 @@ __device__ __forceinline__ uint32_t pick_byte(const u32x4 &d, int pos)
     return (pick_dword(d, pos >> 2) >> (8 * (pos & 3))) & 0xFFu;
 }
 
+// WC_VARIANT (experimental kernel branches for A/B timing, some of which
+// drop results, e.g. bit 64 = no result store) exists only in the tuning
+// build (-DWC_TUNING, libwccksum_tune.so, tools/).  The shipped library
+// compiles every kernel with variant 0, so those branches are folded away and
+// no environment variable can change a result.
+__device__ __forceinline__ constexpr int tuning_variant(int v)
+{
+#ifdef WC_TUNING
+    return v;
+#else
+    return (void)v, 0;
+#endif
+}
+
 // Logical block of this workgroup, XCD-contiguous within super-blocks of
 // 4096 workgroups: workgroups are placed on the 8 XCDs round-robin
 // (blockIdx.x % 8), so inside each super-block XCD x gets logical blocks

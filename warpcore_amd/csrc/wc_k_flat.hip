@@ -1,6 +1,7 @@
 // wc_k_flat.hip -- ragged batches on gfx950: the chunk-balanced flat kernel
-// k_cksum_flat, used for WC_SEG=0 and its diagnostic
-// no-load build; k_cksum_seg falls back to the same tile path.
+// k_cksum_flat, used for WC_SEG=0 and (tuning build
+// only) its diagnostic no-load build; k_cksum_seg falls back to the same tile
+// path.
 #include "wc_flat.h"
 
 namespace wc {
@@ -99,11 +100,14 @@ static hipError_t launch_flat_un(const LaunchArgs &a, hipStream_t st)
     else                                                                       \
         hipLaunchKernelGGL((k_cksum_flat<UN, K, N, H>), dim3(grid), dim3(256), 0, st, b, \
                            a.offs, a.lens, a.n, a.out, bad, a.out_hdr)
+#ifdef WC_TUNING
+    // Diagnostic no-load build (timing only, wrong results): tuning library only.
     if (a.diag_noload && a.kind == WC_KIND_IP) {
         hipLaunchKernelGGL((k_cksum_flat<UN, WC_KIND_IP, true, false, true>), dim3(grid),
                            dim3(256), 0, st, b, a.offs, a.lens, a.n, a.out, bad, a.out_hdr);
         return hipGetLastError();
     }
+#endif
     if (a.kind == WC_KIND_PAYLOAD && a.out_hdr) {
         if (a.nontemporal)
             WC_FLAT(WC_KIND_PAYLOAD, true, true);

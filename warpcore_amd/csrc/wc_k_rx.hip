@@ -1,0 +1,241 @@
+// wc_k_rx.hip -- the RX verdict kernel on gfx950: for every frame of a netmap
+// RX ring (or any batch of Ethernet frames), the checksum and header-format
+// decision the reference's RX path makes, computed on the device from the
+// frame bytes alone.
+//
+// Reference decisions restated (read, not copied):
+//   eth_rx  /root/reference/lib/src/eth.c:77-87     EtherType dispatch
+//   ip4_rx  /root/reference/lib/src/ip4.c:95-138    version, ip_cksum(ip, hl),
+//                                                   fragment offset, protocol
+//   ip6_rx  /root/reference/lib/src/ip6.c:95-110    version, next header
+//   udp_rx  /root/reference/lib/src/udp.c:99-139    ip_plen, MIN(udp->len,
+//           ip_plen), the zero-checksum skip and payload_cksum(ip, udp_len + hl)
+// The codes are enum wc_rx_verdict (include/warpcore_gpu/wc_cksum.h); the CPU
+// restatement is oracle_rx_verdict (oracle/wc_oracle.c).  Engine state (MAC
+// and address filters, bound sockets) stays with the caller.
+//
+// One wave per tile of 64 frames (lane l = frame l), one-shot grid:
+//   1. header fields: two aligned chunks around frame bytes 12..23 (EtherType,
+//      version / IHL, lengths, fragment offset, protocol / next header);
+//   2. with the IHL known: the UDP length and checksum fields, and for IPv4
+//      the header's chunks -- its checksum is summed by the lane itself;
+//   3. the frames whose UDP checksum must be verified go through the gathered
+//      stream of the seg path (wc_seg.h, seg_tile over the tile's IP packets
+//      [ip, ip + udp_len + hl) in packet order), the payload_cksum lanes it
+//      can't take redone exactly by their own lane.
+// Every load stays inside its frame (chunks that overlap [frame, frame +
+// flen) only); whatever the reference would read past the frame is
+// WC_RX_TRUNCATED.  Roofline: HBM, the checked frames' bytes once.
+#include "wc_seg.h"
+
+namespace wc {
+namespace {
+
+// enum wc_rx_verdict (wc_cksum.h)
+constexpr uint32_t kRxOk = 0, kRxOkNoCksum = 1, kRxBadIpCksum = 2, kRxBadUdpCksum = 3,
+                   kRxShort = 4, kRxFragment = 5, kRxBadVersion = 6, kRxNotUdp = 7,
+                   kRxNotIp = 8, kRxTruncated = 9;
+
+__device__ __forceinline__ bool rx_is_drop(uint32_t v)
+{
+    return v != kRxOk && v != kRxOkNoCksum && v != kRxNotUdp && v != kRxNotIp;
+}
+
+struct RxParse {
+    uint64_t ip;      // the frame's IP header (frame + 14)
+    uint32_t plen;    // payload_cksum length udp_len + hl (need)
+    uint32_t verdict; // final unless need
+    bool need;        // the UDP checksum must be verified
+};
+
+// Two aligned chunks holding frame bytes from `at` on, each loaded only if it
+// overlaps the frame (else the zero chunk): never a page the frame does not
+// touch.
+struct Win2 {
+    u32x4 x, y;
+};
+
+__device__ __forceinline__ Win2 win2_load(uint64_t at, uint64_t fend, bool on, uint64_t zero)
+{
+    const uint64_t c = at & ~15ull;
+    Win2 w;
+    w.x = load_chunk<false>(on && c < fend ? c : zero);
+    w.y = load_chunk<false>(on && c + 16u < fend ? c + 16u : zero);
+    return w;
+}
+
+constexpr int kHdrChunks = 5; // an IPv4 header (<= 60 B) at any phase
+
+// Steps 1 and 2 for this lane's frame [fa, fa + flen).  The branch order is
+// the reference's; bytes past the frame only feed decisions that the length
+// checks have already made.
+__device__ __forceinline__ RxParse rx_parse(uint64_t fa, uint32_t flen, bool valid, uint64_t zero)
+{
+    RxParse h{fa + 14u, 0u, kRxTruncated, false};
+    const uint64_t fend = fa + flen;
+    const uint64_t a1 = fa + 12u;
+    const Win2 w1 = win2_load(a1, fend, valid && flen > 12u, zero);
+    const uint32_t s1 = (uint32_t)(a1 & 15u);
+    const uint32_t f0 = win_bytes(w1.x, w1.y, w1.y, s1, 0); // frame 12..15
+    const uint32_t f1 = win_bytes(w1.x, w1.y, w1.y, s1, 1); // frame 16..19 = ip 2..5
+    const uint32_t f2 = win_bytes(w1.x, w1.y, w1.y, s1, 2); // frame 20..23 = ip 6..9
+    const uint32_t etype = ((f0 & 0xFFu) << 8) | ((f0 >> 8) & 0xFFu); // eth.h:44-53
+    const uint32_t b0 = (f0 >> 16) & 0xFFu;                              // vhl / vfc
+    const bool v4 = etype == 0x0800u, v6 = etype == 0x86DDu;
+    const uint32_t room = flen >= 14u ? flen - 14u : 0u; // IP bytes inside the frame
+    const uint32_t hl = v4 ? (b0 & 15u) * 4u : 40u;      // ip4.h:88-92, udp.c:115
+    const bool version_ok = (b0 >> 4) == (v4 ? 4u : 6u);
+    // Header fields (ip4.h:55-66, ip6.h:45-57): valid once the header is in.
+    const bool hdr_in = (v4 || v6) && room >= 1u && version_ok && room >= (v4 ? max(hl, 20u) : 40u);
+    const uint32_t proto = v4 ? f2 >> 24 : f2 & 0xFFu; // p @9 / next_hdr @6
+    // IP4_OFFMASK 0xff1f on the native word @6: the fragment offset (ip4.h:49)
+    const bool frag = v4 && (((f2 & 0x1Fu) | (f2 & 0xFF00u)) != 0u);
+    const uint32_t ip_plen =
+        v4 ? ((((f1 & 0xFFu) << 8) | ((f1 >> 8) & 0xFFu)) - hl) & 0xFFFFu // udp.c:104, wraps
+           : (((f1 >> 16) & 0xFFu) << 8) | (f1 >> 24);                     // udp.c:116
+    const bool udp_in = hdr_in && proto == 17u && ip_plen >= 8u && room >= hl + 8u;
+
+    // Step 2: the UDP length / checksum fields (udp.h:41-46) at ip + hl + 4,
+    // and the IPv4 header's chunks, all issued before any is used.
+    const uint64_t a2 = h.ip + hl + 4u;
+    const Win2 w2 = win2_load(a2, fend, valid && udp_in, zero);
+    const bool hsum = valid && hdr_in && v4;
+    const uint32_t sip = (uint32_t)(h.ip & 15u);
+    const uint64_t cip = h.ip & ~15ull;
+    const uint32_t nh = hsum ? (sip + hl + 15u) >> 4 : 0u;
+    u32x4 hc[kHdrChunks];
+#pragma unroll
+    for (int k = 0; k < kHdrChunks; ++k)
+        hc[k] = load_chunk<false>((uint32_t)k < nh ? cip + 16ull * k : zero);
+    // ip_cksum(ip, hl) (ip4.c:110-115): word sum at even addresses; an odd
+    // start folds rotl32(V, 8) (the seg path's residue identity; <= 30 words,
+    // no wrap).
+    uint32_t V = 0;
+#pragma unroll
+    for (int k = 0; k < kHdrChunks; ++k)
+        V += seg_range(hc[k], 16 * k - (int)sip, 0, (int)hl);
+    const uint16_t ipck = fold_not((h.ip & 1u) ? __builtin_amdgcn_alignbit(V, V, 24) : V);
+    const uint32_t g0 = win_bytes(w2.x, w2.y, w2.y, (uint32_t)(a2 & 15u), 0);
+    const uint32_t ulen = ((g0 & 0xFFu) << 8) | ((g0 >> 8) & 0xFFu);
+    const bool ck_zero = (g0 >> 16) == 0u; // udp.c:132
+    const uint32_t udp_len = min(ulen, ip_plen); // udp.c:126
+    const uint32_t L = udp_len + hl;             // unwrapped; > 65535 is past any frame
+
+    uint32_t v;
+    if (flen < 14u)
+        v = kRxTruncated;
+    else if (!v4 && !v6)
+        v = kRxNotIp;
+    else if (room < 1u)
+        v = kRxTruncated;
+    else if (!version_ok)
+        v = kRxBadVersion;
+    else if (!hdr_in)
+        v = kRxTruncated;
+    else if (v4 && ipck != 0)
+        v = kRxBadIpCksum;
+    else if (frag)
+        v = kRxFragment;
+    else if (proto != 17u)
+        v = kRxNotUdp;
+    else if (ip_plen < 8u)
+        v = kRxShort;
+    else if (!udp_in)
+        v = kRxTruncated;
+    else if (ck_zero)
+        v = kRxOkNoCksum;
+    else if (room < max(L, 20u))
+        v = kRxTruncated;
+    else {
+        v = kRxOk;
+        h.need = valid;
+        h.plen = L;
+    }
+    h.verdict = v;
+    return h;
+}
+
+// UNS: 64-chunk rows per row group of the gathered stream (4, as the seg
+// kernel's ragged default).
+template <int UNS, bool NT>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
+k_rx_verdict(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
+             const uint16_t *__restrict__ flens, uint64_t n, uint8_t *__restrict__ verdict,
+             unsigned long long *__restrict__ drops)
+{
+    struct Lds {
+        FlatLds<UNS> f; // slot table, row marks, prefix sums
+        u32x4 stage[64 * UNS];
+    };
+    __shared__ Lds lds_all[kFlatWaves];
+
+    const int lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
+    Lds &L = lds_all[w];
+    const uint64_t ntiles = (n + 63) / 64;
+    const uint64_t nwaves = (uint64_t)gridDim.x * kFlatWaves;
+    uint64_t tile = xcd_block(13 << 8) * kFlatWaves + w; // the seg kernel's XCD span
+    uint32_t ndrop = 0;
+    const uint64_t zero = (uint64_t)(uintptr_t)&kZeroChunk;
+
+    uint64_t off_n;
+    uint32_t flen_n;
+    meta_load(offs, flens, tile * 64 + lane, n, off_n, flen_n);
+
+    for (; tile < ntiles; tile += nwaves) {
+        const uint64_t p = tile * 64 + lane;
+        const bool valid = p < n;
+        const uint64_t fa = (uint64_t)base + off_n;
+        const uint32_t flen = flen_n;
+        meta_load(offs, flens, (tile + nwaves) * 64 + lane, n, off_n, flen_n);
+
+        const RxParse h = rx_parse(fa, flen, valid, zero);
+        uint32_t v = h.verdict;
+        if (__ballot(h.need)) {
+            // payload_cksum(ip, udp_len + hl) of the frames that need it, as a
+            // gathered stream (every other lane is an empty packet in it).
+            const uint32_t span = h.need ? max(h.plen, 20u) : 0u;
+            const FlatTile t = flat_tile_setup<UNS, 1>(L.f, lane, h.ip, h.plen, span, h.need, 0u);
+            bool done = true;
+            uint16_t rh = 0;
+            uint16_t r = seg_tile<UNS, WC_KIND_PAYLOAD, NT, false, GathSrc<UNS, NT>, true>(
+                L.f.pre, L.stage, lane, h.ip, 16ull * t.cp + (h.ip & 15u), h.plen, h.need,
+                t.total, GathSrc<UNS, NT>{&L.f, t}, zero, done, rh);
+            if (h.need && !done) // header longer than the packet, or a possible wrap
+                r = lane_payload_exact<NT>(h.ip, h.plen);
+            if (h.need)
+                v = r != 0 ? kRxBadUdpCksum : kRxOk; // udp.c:134-139
+            wave_order(); // the tables are rewritten by the next tile
+        }
+        if (valid)
+            verdict[p] = (uint8_t)v;
+        ndrop += valid && rx_is_drop(v);
+    }
+    if (drops) {
+        ndrop = group_sum<64>(ndrop);
+        if (lane == 0 && ndrop)
+            atomicAdd(drops, (unsigned long long)ndrop);
+    }
+}
+
+} // namespace
+
+hipError_t launch_rx_verdict(const void *base, const uint64_t *offs, const uint16_t *flens,
+                             uint64_t n, uint8_t *verdict, uint64_t *drops, bool nt,
+                             hipStream_t st)
+{
+    const uint64_t tiles = (n + 63) / 64;
+    const int grid = (int)std::min<uint64_t>(
+        kMaxGridBlocks, std::max<uint64_t>(1, (tiles + kFlatWaves - 1) / kFlatWaves));
+    if (nt)
+        hipLaunchKernelGGL((k_rx_verdict<4, true>), dim3(grid), dim3(256), 0, st,
+                           (const uint8_t *)base, offs, flens, n, verdict,
+                           (unsigned long long *)drops);
+    else
+        hipLaunchKernelGGL((k_rx_verdict<4, false>), dim3(grid), dim3(256), 0, st,
+                           (const uint8_t *)base, offs, flens, n, verdict,
+                           (unsigned long long *)drops);
+    return hipGetLastError();
+}
+
+} // namespace wc

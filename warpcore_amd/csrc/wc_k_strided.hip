@@ -29,8 +29,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3)))
 k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
         const uint64_t *__restrict__ offs, const uint16_t *__restrict__ lens,
         uint64_t n, uint16_t *__restrict__ out, unsigned long long *__restrict__ bad,
-        uint16_t *__restrict__ out_hdr, int variant)
+        uint16_t *__restrict__ out_hdr, int variant_arg)
 {
+    const int variant = tuning_variant(variant_arg); // 0 outside the tuning build
     static_assert(!(RAGGED && (FULL || HDR)), "ragged group variant: masked, no header");
     static_assert(!HDR || KIND == WC_KIND_PAYLOAD, "header checksum rides on payload");
     static_assert(G >= 4 && G <= 64 && (G & (G - 1)) == 0, "group width");

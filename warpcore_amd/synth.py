@@ -34,6 +34,47 @@ def packed_offsets(lengths: np.ndarray, lead: int = 0) -> np.ndarray:
     return off
 
 
+def make_rx_ring(buf, n: int, ip_lens, slot: int = 2048, v6_every: int = 3):
+    """A netmap RX ring of well-formed UDP frames in `buf` (uint8 device
+    tensor of >= n * slot bytes, already filled with synthetic bytes): frame i
+    in slot i, an Ethernet header (random MACs, EtherType per version,
+    eth.h:44-53) and an IPv4 (IHL 5, DF, no fragment offset) or IPv6 UDP
+    datagram of ip_lens[i] bytes at +14 (stamp_udp_headers), its IPv4 header
+    checksum and UDP checksum computed on the device (wc_cksum_ip_udp_ragged)
+    and stored raw, as mk_ip4_hdr / udp_tx do (ip4.c:184-186, udp.c:209-213).
+    Returns (frame offsets uint64, frame lengths uint16) as numpy arrays."""
+    import torch
+
+    from . import cksum
+
+    dev = buf.device
+    ip_lens = np.asarray(ip_lens, dtype=np.uint16)
+    f_off = (np.arange(n, dtype=np.uint64) * slot).astype(np.uint64)
+    f_len = (ip_lens.astype(np.int64) + 14).astype(np.uint16)
+    d_foff = torch.from_numpy(f_off.astype(np.int64)).to(dev)
+    d_ipoff = d_foff + 14
+    d_iplen = torch.from_numpy(ip_lens.astype(np.int64)).to(dev)
+    stamp_udp_headers(buf, d_ipoff, d_iplen, v6_every=v6_every)
+    v6 = (torch.arange(n, device=dev) % v6_every) == 0
+    # EtherType (network order) and, for IPv4, DF with a zero fragment
+    # offset and a zero header checksum field before it is computed.
+    buf[d_foff + 12] = torch.where(v6, 0x86, 0x08).to(torch.uint8)
+    buf[d_foff + 13] = torch.where(v6, 0xDD, 0x00).to(torch.uint8)
+    o4 = d_ipoff[~v6]
+    for at, val in ((6, 0x40), (7, 0), (10, 0), (11, 0)):
+        buf[o4 + at] = val
+    hdr, pay = cksum.cksum_ip_udp_ragged(buf, d_ipoff.to(torch.int64).view(torch.int64),
+                                         d_iplen.to(torch.int16), check=False)
+    h = hdr.view(torch.int16).to(torch.int32) & 0xFFFF
+    p = pay.view(torch.int16).to(torch.int32) & 0xFFFF
+    buf[o4 + 10] = (h[~v6] & 0xFF).to(torch.uint8)
+    buf[o4 + 11] = (h[~v6] >> 8).to(torch.uint8)
+    ucs = d_ipoff + torch.where(v6, 46, 26)
+    buf[ucs] = (p & 0xFF).to(torch.uint8)
+    buf[ucs + 1] = (p >> 8).to(torch.uint8)
+    return f_off, f_len
+
+
 def stamp_udp_headers(buf, offs, lens, v6_every: int = 3, chunk: int = 1 << 21) -> None:
     """Turn packet i of a synthetic batch into a well-formed UDP datagram in
     place, on the device: IPv6 (every `v6_every`-th packet) or IPv4 with IHL 5
