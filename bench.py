@@ -56,7 +56,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="c2",
-                    choices=["c2", "c3", "c4", "c5", "slots", "zslots", "rx"])
+                    choices=["c2", "c3", "c4", "c5", "slots", "zslots", "rx", "zrx"])
     ap.add_argument("--len", type=int, default=1472, help="packet bytes for c3")
     ap.add_argument("--kind", default="ip", choices=["ip", "payload"],
                     help="ip_cksum (default) or payload_cksum per packet")
@@ -212,6 +212,8 @@ def make_workload(args, dev, rank, world):
                 f"checksums, ip4_rx + udp_rx checks) per frame")
         meta = {"packets_per_gpu": n, "mean_frame_bytes": round(nbytes / n, 2), "slot_bytes": slot,
                 "layout": "ragged", "kind": "rx_verdict"}
+        if args.config == "rx":
+            meta["packet_bytes"] = args.len + 42  # frame: Ethernet 14 + IP/UDP 28 + payload
         plan = {"kernel": "k_rx_verdict (header parse + gathered seg stream)",
                 "grid": int((n + 255) // 256)}
         return step, n, nbytes, buf, out, plan, desc, meta, (f_off, f_len), "weak"

@@ -16,7 +16,10 @@ ROOT = Path(__file__).resolve().parent.parent
 KEYS = {"c2": "c2:1472", "c2pl": "c2:1472:payload:headers", "c4": "c4:zipf",
         "c4pl": "c4:zipf:payload:headers", "slots": "slots:1500",
         "slotspl": "slots:1500:payload:headers", "zslots": "zslots:zipf",
-        "zslotspl": "zslots:zipf:payload:headers"}
+        "zslotspl": "zslots:zipf:payload:headers",
+        "c2f": "c2:1472:payload:headers:fused", "c4f": "c4:zipf:payload:headers:fused",
+        "slotsf": "slots:1500:payload:headers:fused",
+        "zslotsf": "zslots:zipf:payload:headers:fused", "rx": "rx:1514", "zrx": "zrx:zipf"}
 
 
 def main():
@@ -24,11 +27,14 @@ def main():
     go, prof = ROOT / "gpurun_out", ROOT / "profiles"
     traffic = json.loads((prof / "traffic.json").read_text())
     for c in cfgs:
-        key = KEYS.get(c) or "c3:" + c.split("_", 1)[1]
+        key = KEYS.get(c) or "c3:" + c.split("_", 1)[1] + (":payload:headers"
+                                                           if c.startswith("c3pl_") else "")
         shutil.copy(go / "round" / f"bench_{tag}_{c}.json", prof / f"bench_{rnd}_{c}.json")
         shutil.copy(go / f"prof_{tag}_{c}" / "stats" / "run_kernel_stats.csv",
                     prof / f"rocprof_{rnd}_{c}_kernel_stats.csv")
-        alg = traffic[key]["algorithmic_bytes_per_launch"]
+        b = json.loads((go / "round" / f"bench_{tag}_{c}.json").read_text())
+        alg = traffic.get(key, {}).get("algorithmic_bytes_per_launch") or round(
+            b["roofline"]["achieved"] * 1e9 * b["roofline"]["kernel_ms_avg"] * 1e-3)
         subprocess.run([sys.executable, str(ROOT / "tools" / "traffic.py"),
                         str(go / f"prof_{tag}_{c}"), key, "--algorithmic-bytes", str(alg)],
                        check=True, cwd=ROOT, stdout=subprocess.DEVNULL)

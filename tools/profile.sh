@@ -20,6 +20,11 @@ run() {  # $1 = name, rest = rocprofv3 options
     local rc=$?
     echo "$name rc=$rc" | tee -a "$OUT/summary.log"
     case $rc in 0) ;; *) exit $rc ;; esac
+    # keep gpurun_out/ small (it travels back, <= 64 MiB): the per-dispatch
+    # trace is summarised by run_kernel_stats.csv; counters are compressed
+    rm -f "$OUT/$name/run_kernel_trace.csv"
+    [ -f "$OUT/$name/run_counter_collection.csv" ] && gzip -f "$OUT/$name/run_counter_collection.csv"
+    return 0
 }
 
 run stats --kernel-trace --stats

@@ -21,12 +21,20 @@ for c in ${CFGS:-c2 c4 c4pl slotspl}; do
         c3_*) a="--config c3 --len ${c#c3_}" ;;
         zslots) a="--config zslots" ;;
         zslotspl) a="--config zslots --kind payload --headers" ;;
+        c2f) a="--config c2 --fused" ;;
+        c4f) a="--config c4 --fused" ;;
+        slotsf) a="--config slots --fused" ;;
+        zslotsf) a="--config zslots --fused" ;;
+        rx) a="--config rx" ;;
+        zrx) a="--config zrx" ;;
+        c3pl_*) a="--config c3 --len ${c#c3pl_} --kind payload --headers" ;;
         *) echo "unknown config $c"; exit 2 ;;
     esac
     echo "== $c: bench"
-    timeout -k 10 300 python bench.py $a > gpurun_out/round/bench_${TAG}_$c.json \
+    c5=""; [ "$c" = c2 ] || c5="--no-c5"   # the C5 leg rides on the headline line
+    timeout -k 10 300 python bench.py $a $c5 > gpurun_out/round/bench_${TAG}_$c.json \
         2> gpurun_out/round/bench_${TAG}_$c.err || { tail gpurun_out/round/bench_${TAG}_$c.err; exit 1; }
     cat gpurun_out/round/bench_${TAG}_$c.json
     echo "== $c: rocprof"
-    TAG=${TAG}_$c BENCH_ARGS="$a --steps 50 --warmup 5 --no-cpu-baseline" tools/profile.sh || exit 1
+    TAG=${TAG}_$c BENCH_ARGS="$a --steps 50 --warmup 5 --no-cpu-baseline --no-c5" tools/profile.sh || exit 1
 done

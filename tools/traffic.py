@@ -9,14 +9,19 @@ counters are in KiB.
 """
 import argparse
 import csv
+import gzip
 import json
 from pathlib import Path
 
 
 def mean_counter(path: Path, counter: str):
     vals = {}
-    for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] != counter or "k_cksum" not in r["Kernel_Name"]:
+    if not path.exists() and Path(str(path) + ".gz").exists():
+        path = Path(str(path) + ".gz")
+    f = gzip.open(path, "rt") if path.suffix == ".gz" else open(path)
+    for r in csv.DictReader(f):
+        if r["Counter_Name"] != counter or not ("k_cksum" in r["Kernel_Name"]
+                                                or "k_rx_verdict" in r["Kernel_Name"]):
             continue
         vals.setdefault(r["Kernel_Name"].split("(")[0], []).append(float(r["Counter_Value"]))
     name, v = max(vals.items(), key=lambda kv: len(kv[1]))
