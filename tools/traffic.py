@@ -23,7 +23,7 @@ def mean_counter(path: Path, counter: str):
         if r["Counter_Name"] != counter or not ("k_cksum" in r["Kernel_Name"]
                                                 or "k_rx_verdict" in r["Kernel_Name"]):
             continue
-        vals.setdefault(r["Kernel_Name"].split("(")[0], []).append(float(r["Counter_Value"]))
+        vals.setdefault(r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0], []).append(float(r["Counter_Value"]))
     name, v = max(vals.items(), key=lambda kv: len(kv[1]))
     return name, sum(v) / len(v), len(v)
 
