@@ -94,21 +94,21 @@ int wc_cksum_ip_udp_ragged(const void *d_base, const uint64_t *d_off,
 /* --- RX verdict: the reference's RX checks, decided on the device -------- */
 
 /* What the reference's RX path decides for one Ethernet frame from its
- * checksums and header format: eth_rx (eth.c:77-87) -> ip4_rx
- * (ip4.c:95-138) / ip6_rx (ip6.c:95-110) -> udp_rx (udp.c:99-139).  The
+ * checksums and header format: eth_rx (eth.c:75-86) -> ip4_rx
+ * (ip4.c:95-138) / ip6_rx (ip6.c:91-111) -> udp_rx (udp.c:99-139).  The
  * checks run in the reference's order; the first that fails names the code.
- * Engine state -- MAC and IP address filters (eth.c:65-74, ip4.c:103-108,
- * ip6.c:101-104), bound sockets -- is not part of the verdict. */
+ * Engine state -- MAC and IP address filters (eth.c:65-73, ip4.c:103-108,
+ * ip6.c:98-103), bound sockets -- is not part of the verdict. */
 enum wc_rx_verdict {
     WC_RX_OK = 0,            /* UDP, checksum verified (udp.c:134): deliver */
     WC_RX_OK_NO_CKSUM = 1,   /* UDP checksum field 0: accepted unverified (udp.c:132) */
     WC_RX_BAD_IP_CKSUM = 2,  /* ip_cksum(ip, hl) != 0 (ip4.c:110-115): drop */
     WC_RX_BAD_UDP_CKSUM = 3, /* payload_cksum(ip, udp_len + hl) != 0 (udp.c:134-139): drop */
-    WC_RX_SHORT = 4,         /* IP payload shorter than a UDP header (udp.c:121-124): drop */
-    WC_RX_FRAGMENT = 5,      /* IPv4 fragment offset != 0 (ip4.c:122-126): drop */
-    WC_RX_BAD_VERSION = 6,   /* version nibble != the EtherType's (ip4.c:95-98, ip6.c:95-99): drop */
+    WC_RX_SHORT = 4,         /* IP payload shorter than a UDP header (udp.c:123-126): drop */
+    WC_RX_FRAGMENT = 5,      /* IPv4 fragment offset != 0 (ip4.c:123-127): drop */
+    WC_RX_BAD_VERSION = 6,   /* version nibble != the EtherType's (ip4.c:95-98, ip6.c:91-95): drop */
     WC_RX_NOT_UDP = 7,       /* IPv4 / IPv6, another protocol (ICMP, ...): the host's (ip4.c:129-137) */
-    WC_RX_NOT_IP = 8,        /* EtherType neither IPv4 nor IPv6 (ARP, ...): the host's (eth.c:77-87) */
+    WC_RX_NOT_IP = 8,        /* EtherType neither IPv4 nor IPv6 (ARP, ...): the host's (eth.c:75-86) */
     WC_RX_TRUNCATED = 9,     /* a byte the reference reads lies past the frame: drop */
 };
 #define WC_RX_IS_DROP(v) \
@@ -230,6 +230,12 @@ int wc_synth_fill(void *d_buf, uint64_t nbytes, uint64_t seed, void *stream);
 int wc_plan_strided(uint64_t base_addr, uint64_t stride, uint16_t len,
                     uint64_t n, int kind, int *group, int *chunks_per_lane,
                     int *unroll, int *grid);
+
+/* Which kernel family the dispatcher picks for that strided batch: "lean"
+ * (aligned, one pass per packet), "group" (group-per-packet) or "seg"
+ * (segmented-prefix stream of a packed batch). */
+const char *wc_plan_strided_kernel(uint64_t base_addr, uint64_t stride, uint16_t len,
+                                   uint64_t n, int kind);
 
 const char *wc_strerror(int err);
 const char *wc_version(void);

@@ -64,8 +64,8 @@ RX_DROPS = {RX_BAD_IP_CKSUM, RX_BAD_UDP_CKSUM, RX_SHORT, RX_FRAGMENT, RX_BAD_VER
 
 def rx_verdict(frame: bytes, flen: int | None = None) -> int:
     """The checksum / format decision of the reference's RX path for one
-    Ethernet frame: eth_rx (eth.c:77-87) -> ip4_rx (ip4.c:95-138) / ip6_rx
-    (ip6.c:95-110) -> udp_rx (udp.c:99-139).  Only frame bytes [0, flen) are
+    Ethernet frame: eth_rx (eth.c:75-86) -> ip4_rx (ip4.c:95-138) / ip6_rx
+    (ip6.c:91-111) -> udp_rx (udp.c:99-139).  Only frame bytes [0, flen) are
     read; whatever the reference would read past them is RX_TRUNCATED."""
     f = bytes(frame)
     flen = len(f) if flen is None else flen

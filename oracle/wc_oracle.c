@@ -179,7 +179,7 @@ static inline uint16_t be16_at(const uint8_t *p) { return (uint16_t)((p[0] << 8)
 
 int oracle_rx_verdict(const uint8_t *f, uint16_t flen)
 {
-    /* eth_rx (eth.c:77-87): dispatch on the EtherType @12 (eth.h:44-53). */
+    /* eth_rx (eth.c:75-86): dispatch on the EtherType @12 (eth.h:44-53). */
     if (flen < 14)
         return RX_TRUNCATED;
     const uint16_t type = be16_at(f + 12);
@@ -190,7 +190,7 @@ int oracle_rx_verdict(const uint8_t *f, uint16_t flen)
     if (room < 1)
         return RX_TRUNCATED;
     const int v4 = type == 0x0800;
-    /* ip4_rx / ip6_rx: version nibble (ip4.c:95-98, ip6.c:95-99, ip4.h:75-79) */
+    /* ip4_rx / ip6_rx: version nibble (ip4.c:95-98, ip6.c:91-95, ip4.h:75-79) */
     if ((ip[0] >> 4) != (v4 ? 4 : 6))
         return RX_BAD_VERSION;
     uint32_t hl, ip_plen, proto;
@@ -203,28 +203,28 @@ int oracle_rx_verdict(const uint8_t *f, uint16_t flen)
         if (oracle_ip_cksum(ip, (uint16_t)hl) != 0) /* ip4.c:110-115 */
             return RX_BAD_IP_CKSUM;
         /* ip->off & IP4_OFFMASK (0xff1f in network order, ip4.h:49): the
-         * 13-bit fragment offset; the MF flag alone passes (ip4.c:122-126). */
+         * 13-bit fragment offset; the MF flag alone passes (ip4.c:123-127). */
         if ((ip[6] & 0x1Fu) || ip[7])
             return RX_FRAGMENT;
         proto = ip[9];
         /* udp.c:104: uint16 arithmetic, wraps when len < hl */
         ip_plen = (uint16_t)(be16_at(ip + 2) - hl);
     } else {
-        hl = 40; /* sizeof(struct ip6_hdr), udp.c:115 */
+        hl = 40; /* sizeof(struct ip6_hdr), udp.c:113 */
         if (room < 40)
             return RX_TRUNCATED;
         proto = ip[6];          /* next_hdr, ip6.c:105 */
-        ip_plen = be16_at(ip + 4); /* udp.c:116 */
+        ip_plen = be16_at(ip + 4); /* udp.c:114 */
     }
     if (proto != 17) /* IP_P_UDP: ICMP and the rest go elsewhere */
         return RX_NOT_UDP;
-    if (ip_plen < 8) /* udp.c:121-124 */
+    if (ip_plen < 8) /* udp.c:123-126 */
         return RX_SHORT;
     if (room < hl + 8) /* the UDP header (udp.h:41-46) at ip + hl */
         return RX_TRUNCATED;
     const uint8_t *udp = ip + hl;
     const uint32_t ulen = be16_at(udp + 4);
-    const uint32_t udp_len = ulen < ip_plen ? ulen : ip_plen; /* udp.c:126 */
+    const uint32_t udp_len = ulen < ip_plen ? ulen : ip_plen; /* udp.c:128 */
     if (udp[6] == 0 && udp[7] == 0) /* udp.c:132: no checksum, accepted */
         return RX_OK_NO_CKSUM;
     /* payload_cksum(ip, udp_len + hl) reads [0, max(len, 20)) -- the length

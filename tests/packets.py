@@ -123,7 +123,7 @@ RX_CASES = ("ok4", "ok6", "ok4opt", "nocksum", "badudp", "badip", "frag", "mf", 
 
 def rx_frame(rng: np.random.Generator, case: str, max_payload: int = 1472) -> tuple[bytes, int]:
     """One Ethernet frame of an RX ring exercising `case` of the reference's
-    RX checks (ip4.c:95-138, ip6.c:95-110, udp.c:99-139); returns (bytes,
+    RX checks (ip4.c:95-138, ip6.c:91-111, udp.c:99-139); returns (bytes,
     frame length), the length possibly shorter than the bytes (a truncated
     slot: what lies past it is not part of the frame)."""
     plen = int(rng.integers(0, max_payload + 1))
@@ -153,12 +153,12 @@ def rx_frame(rng: np.random.Generator, case: str, max_payload: int = 1472) -> tu
         pkt, _ = ipv4_udp(payload, rng, ihl=ihl, proto=1 if case == "icmp4" else 17)
     b = bytearray(pkt)
     hl = 40 if v6 else ihl * 4
-    if case == "short":  # IP payload < 8 (udp.c:121-124)
+    if case == "short":  # IP payload < 8 (udp.c:123-126)
         if v6:
             b[4:6] = _u16be(int(rng.integers(0, 8)))
         else:
             b[2:4] = _u16be(hl + int(rng.integers(0, 8)))
-    if case == "ulen_big":  # udp->len > ip_plen: MIN() takes ip_plen (udp.c:126)
+    if case == "ulen_big":  # udp->len > ip_plen: MIN() takes ip_plen (udp.c:128)
         b[hl + 4:hl + 6] = _u16be(int(rng.integers(len(b) - hl + 1, 65536)))
     if case == "ulen_small":  # udp->len < 8 or shorter than the datagram
         b[hl + 4:hl + 6] = _u16be(int(rng.integers(0, max(9, len(b) - hl))))

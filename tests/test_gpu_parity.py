@@ -977,3 +977,64 @@ def test_production_lib_ignores_tuning_knobs(gpu, monkeypatch):
         np.testing.assert_array_equal(host(got), c_oracle.cksum_ragged(d[:total].cpu().numpy(),
                                                                        offs, lens, kind=k))
     del d
+
+
+LEAN_LENS = [16, 32, 48, 64, 80, 96, 128, 144, 192, 256, 320, 512, 576, 768]
+
+
+@pytest.mark.parametrize("length", LEAN_LENS)
+@pytest.mark.parametrize("shape", ["", "4,1,2", "8,2,2", "16,3,2", "32,4,1"])
+def test_lean_kernel_aligned(gpu, monkeypatch, length, shape):
+    """Aligned strided batches through the lean kernel (wc_k_lean.hip): both
+    kinds, tail waves (n not a multiple of a wave's packets), packets that do
+    not fill their group's pass, and payload_cksum over well-formed IPv4 /
+    IPv6 UDP headers, IPv4 options, IHL < 5 and random header bytes (the
+    lanes recomputed exactly)."""
+    for k in ("WC_SHAPE", "WC_STRIDED_SEG", "WC_LEAN_MAX"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("WC_LEAN_MAX", "64")
+    if shape:
+        monkeypatch.setenv("WC_SHAPE", shape)
+    wc.reload_config()
+    G, C, U = (int(x) for x in shape.split(",")) if shape else (0, 0, 0)
+    if shape and length // 16 > G * C:
+        pytest.skip("shape does not cover the packet in one pass")
+    rng = np.random.default_rng(length + 7 * G + C)
+    for stride in (length, length + 16, 2048):
+        for n in (1, 63, 1000 + G):
+            buf = rng.integers(0, 256, n * stride + 64, dtype=np.uint8)
+            d = dev_u8(buf, gpu)
+            assert wc.plan_strided(d.data_ptr(), stride, length, n)["kernel"] == "lean"
+            got = host(wc.cksum_strided(d, stride, length, n, kind="ip"))
+            np.testing.assert_array_equal(got, c_oracle.cksum_strided(buf, stride, length, n),
+                                          err_msg=f"ip stride {stride} n {n}")
+            if length < 48:
+                continue
+            hb = buf.copy()
+            for i in range(n):
+                o = i * stride
+                r = i % 5
+                if r == 4:
+                    continue  # random bytes as the header
+                pl = rng.integers(0, 256, max(0, length - 48), dtype=np.uint8).tobytes()
+                if r == 0:
+                    pkt, _ = ipv6_udp(pl + bytes(max(0, 48 - 48)), rng)
+                elif r == 1:
+                    pkt, _ = ipv4_udp(pl + bytes(20), rng, ihl=int(rng.integers(6, 11)))
+                elif r == 2:
+                    pkt, _ = ipv4_udp(pl + bytes(20), rng)
+                    pkt = bytes([0x40 | int(rng.integers(0, 5))]) + pkt[1:]
+                else:
+                    pkt, _ = ipv4_udp(pl + bytes(20), rng)
+                pkt = pkt[:length]
+                hb[o:o + len(pkt)] = np.frombuffer(pkt, np.uint8)
+            d = dev_u8(hb, gpu)
+            assert wc.plan_strided(d.data_ptr(), stride, length, n,
+                                   kind="payload")["kernel"] == "lean"
+            got = host(wc.cksum_strided(d, stride, length, n, kind="payload"))
+            np.testing.assert_array_equal(got, c_oracle.cksum_strided(hb, stride, length, n,
+                                                                      kind=1),
+                                          err_msg=f"payload stride {stride} n {n}")
+            out, bad = wc.verify_strided(d, stride, length, n, kind="payload")
+            assert int(bad.item()) == int((c_oracle.cksum_strided(hb, stride, length, n,
+                                                                  kind=1) != 0).sum())

@@ -1,6 +1,6 @@
 """RX verdicts on the GPU (wc_rx_verdict_ragged / wc_rx_verdict_host) against
 the oracle's restatement of the reference's RX checks (oracle_rx_verdict:
-eth.c:77-87, ip4.c:95-138, ip6.c:95-110, udp.c:99-139) -- every frame, exact
+eth.c:75-86, ip4.c:95-138, ip6.c:91-111, udp.c:99-139) -- every frame, exact
 code.
 
 Layouts: a netmap RX ring (one frame per 2048-B slot buffer, slots listed in

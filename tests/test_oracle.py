@@ -147,8 +147,8 @@ def test_strided_matches_scalar():
 
 
 # ---------------------------------------------------------------------------
-# RX verdicts: the reference's RX checks (eth.c:77-87, ip4.c:95-138,
-# ip6.c:95-110, udp.c:99-139), two independent restatements.
+# RX verdicts: the reference's RX checks (eth.c:75-86, ip4.c:95-138,
+# ip6.c:91-111, udp.c:99-139), two independent restatements.
 
 def test_rx_verdict_c_vs_py_every_case():
     rng = np.random.default_rng(11)
@@ -179,7 +179,7 @@ def test_rx_verdict_reference_details():
     b[14 + 6:14 + 8] = b"\x20\x00"
     fr = eth_frame(finish_udp(bytes(b[14:])), rng)
     assert v.rx_verdict(fr) == v.RX_OK == c_oracle.rx_verdict(fr)
-    # a fragment offset (low 5 bits of byte 6 or byte 7) is dropped (ip4.c:122)
+    # a fragment offset (low 5 bits of byte 6 or byte 7) is dropped (ip4.c:123)
     b = bytearray(f[14:])
     b[7] = 1
     fr = eth_frame(finish_udp(bytes(b)), rng)
@@ -197,13 +197,13 @@ def test_rx_verdict_reference_details():
     # the frame ends inside the UDP payload: the reference would read past it
     assert v.rx_verdict(f, len(f) - 1) == v.RX_TRUNCATED == c_oracle.rx_verdict(f, len(f) - 1)
     # udp->len shorter than the datagram: only udp_len + hl is summed
-    # (udp.c:126, 134), so bytes after it do not matter
+    # (udp.c:128, 134), so bytes after it do not matter
     pkt, _ = ipv4_udp(b"z" * 64, rng)
     b = bytearray(pkt)
     b[20 + 4:20 + 6] = (8 + 10).to_bytes(2, "big")
     fr = bytearray(eth_frame(finish_udp(bytes(b)), rng))
     fr[14 + 20 + 8 + 30] ^= 0x55
     assert v.rx_verdict(bytes(fr)) == v.RX_OK == c_oracle.rx_verdict(bytes(fr))
-    # ARP and the rest go to the host (eth.c:77-87)
+    # ARP and the rest go to the host (eth.c:75-86)
     arp = bytes(12) + b"\x08\x06" + bytes(28)
     assert v.rx_verdict(arp) == v.RX_NOT_IP == c_oracle.rx_verdict(arp)

@@ -51,6 +51,7 @@ SIGNATURES = {
     "wc_plan_strided": (_int, [_u64, _u64, _u16, _u64, _int,
                                ctypes.POINTER(_int), ctypes.POINTER(_int),
                                ctypes.POINTER(_int), ctypes.POINTER(_int)]),
+    "wc_plan_strided_kernel": (ctypes.c_char_p, [_u64, _u64, _u16, _u64, _int]),
     "wc_strerror": (ctypes.c_char_p, [_int]),
     "wc_version": (ctypes.c_char_p, []),
 }

@@ -419,7 +419,10 @@ def plan_strided(base_addr: int, stride: int, length: int, n: int, kind="ip") ->
     vals = [ctypes.c_int() for _ in range(4)]
     _check("wc_plan_strided", _lib.load().wc_plan_strided(
         base_addr, stride, length, n, _kind(kind), *[ctypes.byref(v) for v in vals]))
-    return dict(zip(("group", "chunks_per_lane", "unroll", "grid"), (v.value for v in vals)))
+    plan = dict(zip(("group", "chunks_per_lane", "unroll", "grid"), (v.value for v in vals)))
+    plan["kernel"] = _lib.load().wc_plan_strided_kernel(base_addr, stride, length, n,
+                                                        _kind(kind)).decode()
+    return plan
 
 
 def gpu_init(device: int = -1) -> None:

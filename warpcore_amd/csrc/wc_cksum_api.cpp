@@ -120,6 +120,7 @@ struct Config {
     int grp_rows = 4;              // WC_GRP_ROWS
     int flat_pk = 1;               // WC_FLAT_PK: flat kernel chunks per lane slot
     int gather = 1;                // WC_GATHER: seg kernel's gathered-stream path (0 off, 2 forced)
+    int lean_max = 48;             // WC_LEAN_MAX: lean kernel for aligned packets up to this many chunks
 };
 
 std::mutex g_mu;
@@ -194,6 +195,7 @@ void load_config_locked()
     c.grp_rows = env_int("WC_GRP_ROWS", c.grp_rows);
     c.flat_pk = env_int("WC_FLAT_PK", c.flat_pk);
     c.gather = env_int("WC_GATHER", c.gather);
+    c.lean_max = env_int("WC_LEAN_MAX", c.lean_max);
     g_cfg = c;
     g_cfg_loaded = true;
 }
@@ -355,7 +357,18 @@ struct Plan {
     bool full;
     int grid;
     int seg_rows = 0; // ragged: k_cksum_seg row-group size, 0 = flat kernel
+    bool lean = false; // aligned strided, one pass per packet: k_cksum_lean
 };
+
+bool lean_shape_ok(const wc::Shape &sh)
+{
+#define WC_SHAPE(G_, C_, U_)                                                   \
+    if (sh.group == G_ && sh.cpl == C_ && sh.unroll == U_)                     \
+        return true;
+    WC_LEAN_SHAPE_LIST
+#undef WC_SHAPE
+    return false;
+}
 
 Plan plan_strided(const Device &D, const Config &C, uint64_t base, uint64_t stride,
                   uint32_t len, uint64_t n, int kind, bool hdr = false)
@@ -407,6 +420,24 @@ Plan plan_strided(const Device &D, const Config &C, uint64_t base, uint64_t stri
         p.seg_rows = C.seg_rows_set ? C.seg_rows : (nch <= rows2 ? 2 : 4);
         p.grid = 0;
     }
+    // Aligned packets (base, stride and len multiples of 16) that one pass of
+    // a group covers take the lean kernel (wc_k_lean.hip): scalar wave
+    // addresses, word sums, payload_cksum's header terms from the group's
+    // first lane.  payload_cksum needs len >= 48 there (the whole IPv4 /
+    // IPv6 header inside the packet); up to WC_LEAN_MAX chunks.
+    const bool aligned16 = base % 16 == 0 && stride % 16 == 0 && len % 16 == 0 && len != 0;
+    if (!hdr && C.lean_max > 0 && aligned16 && (!payload || len >= 48) &&
+        nch <= (uint32_t)C.lean_max && (sseg != 2 || !packed)) {
+        const wc::Shape sh = C.have_shape ? C.shape : shape_for_chunks(nch, true, false, true);
+        const uint64_t ppw = (uint64_t)(64 / std::max(sh.group, 1)) * sh.unroll;
+        if (lean_shape_ok(sh) && nch <= (uint32_t)(sh.group * sh.cpl) && ppw <= 64 &&
+            ppw * stride < (1ull << 32)) {
+            p.shape = sh;
+            p.lean = true;
+            p.seg_rows = 0;
+            p.grid = grid_for(D, C, sh, n);
+        }
+    }
     return p;
 }
 
@@ -454,8 +485,9 @@ int run(const Device &D, const Config &C, const wc::LaunchArgs &args, const Plan
     a.grp_rows = C.grp_rows;
     a.flat_pk = C.flat_pk;
     a.gather = C.gather;
-    hipError_t e = p.shape.group == 0 ? wc::launch_flat(a, p.shape.unroll, st)
-                                      : wc::launch_cksum(a, p.shape, p.grid, st);
+    hipError_t e = p.lean              ? wc::launch_lean(a, p.shape, p.grid, st)
+                   : p.shape.group == 0 ? wc::launch_flat(a, p.shape.unroll, st)
+                                        : wc::launch_cksum(a, p.shape, p.grid, st);
     return hip_err(e);
 }
 
@@ -1502,6 +1534,19 @@ int wc_plan_strided(uint64_t base_addr, uint64_t stride, uint16_t len,
     if (grid)
         *grid = p.grid;
     return WC_OK;
+}
+
+const char *wc_plan_strided_kernel(uint64_t base_addr, uint64_t stride, uint16_t len, uint64_t n,
+                                   int kind)
+{
+    if (kind != WC_CKSUM_IP && kind != WC_CKSUM_PAYLOAD)
+        return "invalid";
+    Device *D = nullptr;
+    Config C;
+    if (ensure_device(&D, &C))
+        return "invalid";
+    const Plan p = plan_strided(*D, C, base_addr, stride, len, n, kind);
+    return p.lean ? "lean" : p.shape.group == 0 ? "seg" : "group";
 }
 
 const char *wc_strerror(int err)

@@ -73,6 +73,36 @@
     WC_SHAPE(64, 4, 1)                                                         \
     WC_SHAPE(16, 6, 4)
 
+// Shapes of the lean kernel (aligned strided batches, one pass per packet;
+// wc_k_lean.hip): the planner's FULL shapes up to 576 B plus tuning
+// neighbours for small packets.
+#define WC_LEAN_SHAPE_LIST                                                     \
+    WC_SHAPE(4, 1, 2)                                                          \
+    WC_SHAPE(4, 1, 4)                                                          \
+    WC_SHAPE(4, 2, 2)                                                          \
+    WC_SHAPE(4, 2, 4)                                                          \
+    WC_SHAPE(8, 1, 2)                                                          \
+    WC_SHAPE(8, 1, 4)                                                          \
+    WC_SHAPE(8, 1, 8)                                                          \
+    WC_SHAPE(8, 2, 2)                                                          \
+    WC_SHAPE(8, 2, 4)                                                          \
+    WC_SHAPE(8, 3, 2)                                                          \
+    WC_SHAPE(8, 6, 1)                                                          \
+    WC_SHAPE(16, 1, 4)                                                         \
+    WC_SHAPE(16, 2, 2)                                                         \
+    WC_SHAPE(16, 2, 4)                                                         \
+    WC_SHAPE(16, 3, 1)                                                         \
+    WC_SHAPE(16, 3, 2)                                                         \
+    WC_SHAPE(16, 6, 2)                                                         \
+    WC_SHAPE(32, 2, 2)                                                         \
+    WC_SHAPE(32, 2, 4)                                                         \
+    WC_SHAPE(32, 3, 1)                                                         \
+    WC_SHAPE(32, 3, 2)                                                         \
+    WC_SHAPE(32, 4, 1)                                                         \
+    WC_SHAPE(32, 4, 2)                                                         \
+    WC_SHAPE(32, 18, 1)                                                        \
+    WC_SHAPE(64, 4, 1)
+
 namespace wc {
 
 // Largest grid any launcher uses: gridDim.x * 256 threads must fit in a
@@ -117,6 +147,8 @@ struct Shape {
 // variant over WC_RAGGED_SHAPE_LIST.
 hipError_t launch_cksum(const LaunchArgs &a, const Shape &sh, int grid,
                         hipStream_t st);
+// Aligned strided batches, one pass per packet (wc_k_lean.hip).
+hipError_t launch_lean(const LaunchArgs &a, const Shape &sh, int grid, hipStream_t st);
 // Ragged batches: a.seg_rows != 0 -> the segmented-prefix kernel (dense
 // tiles; the rest take its flat path), else the chunk-balanced flat kernel
 // (rows = 64-chunk rows per ping-pong group: 1, 2 or 4).

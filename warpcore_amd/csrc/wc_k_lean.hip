@@ -1,0 +1,188 @@
+// wc_k_lean.hip -- aligned strided batches whose packets fit one pass of the
+// group: the lean group kernel k_cksum_lean.
+//
+// Preconditions (wc_cksum_api.cpp plan_strided): base, stride and len are
+// multiples of 16, len / 16 <= G * CPL, PPW * stride < 2^32, and for
+// payload_cksum len >= 48.  Every chunk is then a whole 16-byte chunk of one
+// packet, every packet starts at an even address, and the reference's
+// accumulator is a plain word sum:
+//   ip_cksum       V = the little-endian words of [0, len)      (in_cksum.c:107-120)
+//   payload_cksum  V = words of [8, len) + per-packet terms      (in_cksum.c:140-164)
+// where the per-packet terms (payload_as_ip in wc_flat.h: IPv4 with IHL 5
+// minus bytes 8..11 plus proto << 8, IPv6 plus the payload-length word,
+// then the plen re-swap / next_hdr << 24) come from the packet's first chunk,
+// which the group's lane 0 holds -- no cross-lane header exchange.  A packet
+// those terms do not cover (IPv4 with options or IHL < 5) is recomputed
+// exactly by the lane that stores its result (lane_payload_exact).
+//
+// What makes it lean: the wave's first packet address is scalar (SGPRs), each
+// lane's chunk is a 32-bit offset from it (global_load ... saddr), so the
+// prologue before the first load is a handful of instructions; 4 v_dot2 per
+// chunk instead of 8 v_dot4 byte-lane sums; no masks unless the tail wave or
+// a pass the packet does not fill needs them.  Tiny packets are the case it
+// is for: C3 64 B spends most of a wave's life before its first load and
+// after its last (profiles/ab_r02_lane_store.log).
+#include "wc_seg.h"
+
+namespace wc {
+namespace {
+
+typedef const uint8_t __attribute__((address_space(1))) *gbyte_ptr;
+
+template <bool NT>
+__device__ __forceinline__ u32x4 load_at(gbyte_ptr b, uint32_t off)
+{
+    gchunk_ptr p = (gchunk_ptr)(b + off);
+    if constexpr (NT)
+        return __builtin_nontemporal_load(p);
+    else
+        return *p;
+}
+
+__device__ __forceinline__ uint32_t wsum4(const u32x4 &d, uint32_t acc)
+{
+    return wsum(d.w, wsum(d.z, wsum(d.y, wsum(d.x, acc))));
+}
+
+// payload_cksum's per-packet terms from the packet's first chunk c (bytes
+// 0..15), for the word sum over [8, len): see payload_as_ip (wc_flat.h).
+// ok = false for an IPv4 header that is not 20 bytes long.
+__device__ __forceinline__ uint32_t lean_extra(const u32x4 &c, bool &ok)
+{
+    const uint32_t b0 = c.x & 0xFFu;
+    const PseudoHdr ph = pseudo_hdr(b0, (c.x >> 16) & 0xFFu, c.x >> 24, (c.y >> 16) & 0xFFu);
+    ok = !ph.v4 || ph.hl == 20u;
+    return ph.v4 ? ph.special - ((c.z & 0xFFu) + ((c.z >> 16) & 0xFFu) + ((c.z >> 24) << 8))
+                 : ph.special + (c.y & 0xFFFFu);
+}
+
+template <int G, int CPL, int U, int KIND, bool NT>
+__global__ void __launch_bounds__(256)
+k_cksum_lean(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len, uint64_t n,
+             uint16_t *__restrict__ out, unsigned long long *__restrict__ bad, int variant_arg)
+{
+    const int variant = tuning_variant(variant_arg); // 0 outside the tuning build
+    constexpr int GPW = 64 / G;
+    constexpr uint32_t PPW = (uint32_t)GPW * U;
+    constexpr uint32_t PASS = (uint32_t)G * CPL;
+    constexpr bool PL = KIND == WC_KIND_PAYLOAD;
+    static_assert(PPW <= 64, "one result store per wave-iteration");
+
+    const int lane = threadIdx.x & 63;
+    const uint32_t gl = (uint32_t)lane & (G - 1u);
+    const uint32_t grp = (uint32_t)lane / G;
+    // Wave-uniform in SGPRs: the wave index and so the first packet's address.
+    const uint32_t wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
+    const uint32_t nch = len >> 4;
+    const bool fills = nch == PASS; // uniform: every chunk slot holds packet bytes
+    const uint32_t lo = grp * (uint32_t)stride + 16u * gl;
+    const uint32_t ustep = (uint32_t)GPW * (uint32_t)stride;
+    uint32_t nbad = 0;
+
+    for (uint64_t wave = xcd_block(variant) * 4u + wib; wave * PPW < n; wave += nwaves) {
+        const uint64_t p0 = wave * PPW;
+        const gbyte_ptr gb = (gbyte_ptr)(base + p0 * stride);
+        u32x4 d[U][CPL];
+        if (fills && p0 + PPW <= n) { // uniform: no masks
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int c = 0; c < CPL; ++c)
+                    d[u][c] = load_at<NT>(gb, lo + (uint32_t)u * ustep + 16u * G * c);
+        } else {
+            // The tail wave, or a pass the packets do not fill: a dead slot
+            // re-reads the wave's first chunk (inside the batch) and is zeroed.
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int c = 0; c < CPL; ++c) {
+                    const bool live =
+                        p0 + (uint64_t)u * GPW + grp < n && gl + (uint32_t)c * G < nch;
+                    const u32x4 x =
+                        load_at<NT>(gb, live ? lo + (uint32_t)u * ustep + 16u * G * c : 0u);
+                    d[u][c] = live ? x : u32x4{0u, 0u, 0u, 0u};
+                }
+        }
+        if constexpr (CPL * U < 16)
+            __builtin_amdgcn_sched_barrier(0); // every load before the first sum
+
+        uint32_t res = 0;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            uint32_t V = 0;
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) {
+                if (PL && c == 0) // payload_cksum sums from byte 8 on
+                    V = gl == 0 ? wsum(d[u][0].w, wsum(d[u][0].z, V)) : wsum4(d[u][0], V);
+                else
+                    V = wsum4(d[u][c], V);
+            }
+            uint32_t flag = 0;
+            if constexpr (PL) {
+                bool ok = true;
+                const uint32_t extra = lean_extra(d[u][0], ok);
+                V += gl == 0 ? extra : 0u;
+                flag = ok ? 0u : 0x10000u;
+            }
+            V = group_sum<G>(V);
+            // Lane j of the wave takes packet p0 + j's result from its group
+            // leader (the leader's header flag rides in bit 16).
+            const int src = (lane % GPW) * G;
+            const uint32_t r = __shfl((uint32_t)fold_not(V) | flag, src, 64);
+            if (lane / GPW == u)
+                res = r;
+        }
+        const uint64_t i = p0 + (uint64_t)lane;
+        if (lane < (int)PPW && i < n) {
+            uint16_t r = (uint16_t)res;
+            if constexpr (PL)
+                if (res >> 16) // IPv4 header with options / IHL < 5: exact, by this lane
+                    r = lane_payload_exact<NT>((uint64_t)base + i * stride, len);
+            if (out)
+                out[i] = r;
+            nbad += r != 0;
+        }
+    }
+    if (bad) {
+        nbad = group_sum<64>(nbad);
+        if (lane == 0 && nbad)
+            atomicAdd(bad, (unsigned long long)nbad);
+    }
+}
+
+template <int G, int CPL, int U>
+hipError_t launch_lean_shape(const LaunchArgs &a, int grid, hipStream_t st)
+{
+#define WC_LEAN_K(K, N)                                                        \
+    hipLaunchKernelGGL((k_cksum_lean<G, CPL, U, K, N>), dim3(grid), dim3(256), 0, st,   \
+                       (const uint8_t *)a.base, a.stride, a.len, a.n, a.out,           \
+                       (unsigned long long *)a.bad, a.variant)
+    if (a.kind == WC_KIND_PAYLOAD) {
+        if (a.nontemporal)
+            WC_LEAN_K(WC_KIND_PAYLOAD, true);
+        else
+            WC_LEAN_K(WC_KIND_PAYLOAD, false);
+    } else {
+        if (a.nontemporal)
+            WC_LEAN_K(WC_KIND_IP, true);
+        else
+            WC_LEAN_K(WC_KIND_IP, false);
+    }
+#undef WC_LEAN_K
+    return hipGetLastError();
+}
+
+} // namespace
+
+hipError_t launch_lean(const LaunchArgs &a, const Shape &sh, int grid, hipStream_t st)
+{
+#define WC_SHAPE(G_, C_, U_)                                                   \
+    if (sh.group == G_ && sh.cpl == C_ && sh.unroll == U_)                     \
+        return launch_lean_shape<G_, C_, U_>(a, grid, st);
+    WC_LEAN_SHAPE_LIST
+#undef WC_SHAPE
+    return hipErrorInvalidValue;
+}
+
+} // namespace wc

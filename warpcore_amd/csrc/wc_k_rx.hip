@@ -4,10 +4,10 @@
 // frame bytes alone.
 //
 // Reference decisions restated (read, not copied):
-//   eth_rx  /root/reference/lib/src/eth.c:77-87     EtherType dispatch
+//   eth_rx  /root/reference/lib/src/eth.c:75-86     EtherType dispatch
 //   ip4_rx  /root/reference/lib/src/ip4.c:95-138    version, ip_cksum(ip, hl),
 //                                                   fragment offset, protocol
-//   ip6_rx  /root/reference/lib/src/ip6.c:95-110    version, next header
+//   ip6_rx  /root/reference/lib/src/ip6.c:91-111    version, next header
 //   udp_rx  /root/reference/lib/src/udp.c:99-139    ip_plen, MIN(udp->len,
 //           ip_plen), the zero-checksum skip and payload_cksum(ip, udp_len + hl)
 // The codes are enum wc_rx_verdict (include/warpcore_gpu/wc_cksum.h); the CPU
@@ -83,7 +83,7 @@ __device__ __forceinline__ RxParse rx_parse(uint64_t fa, uint32_t flen, bool val
     const uint32_t b0 = (f0 >> 16) & 0xFFu;                              // vhl / vfc
     const bool v4 = etype == 0x0800u, v6 = etype == 0x86DDu;
     const uint32_t room = flen >= 14u ? flen - 14u : 0u; // IP bytes inside the frame
-    const uint32_t hl = v4 ? (b0 & 15u) * 4u : 40u;      // ip4.h:88-92, udp.c:115
+    const uint32_t hl = v4 ? (b0 & 15u) * 4u : 40u;      // ip4.h:88-92, udp.c:113
     const bool version_ok = (b0 >> 4) == (v4 ? 4u : 6u);
     // Header fields (ip4.h:55-66, ip6.h:45-57): valid once the header is in.
     const bool hdr_in = (v4 || v6) && room >= 1u && version_ok && room >= (v4 ? max(hl, 20u) : 40u);
@@ -92,7 +92,7 @@ __device__ __forceinline__ RxParse rx_parse(uint64_t fa, uint32_t flen, bool val
     const bool frag = v4 && (((f2 & 0x1Fu) | (f2 & 0xFF00u)) != 0u);
     const uint32_t ip_plen =
         v4 ? ((((f1 & 0xFFu) << 8) | ((f1 >> 8) & 0xFFu)) - hl) & 0xFFFFu // udp.c:104, wraps
-           : (((f1 >> 16) & 0xFFu) << 8) | (f1 >> 24);                     // udp.c:116
+           : (((f1 >> 16) & 0xFFu) << 8) | (f1 >> 24);                     // udp.c:114
     const bool udp_in = hdr_in && proto == 17u && ip_plen >= 8u && room >= hl + 8u;
 
     // Step 2: the UDP length / checksum fields (udp.h:41-46) at ip + hl + 4,
@@ -118,7 +118,7 @@ __device__ __forceinline__ RxParse rx_parse(uint64_t fa, uint32_t flen, bool val
     const uint32_t g0 = win_bytes(w2.x, w2.y, w2.y, (uint32_t)(a2 & 15u), 0);
     const uint32_t ulen = ((g0 & 0xFFu) << 8) | ((g0 >> 8) & 0xFFu);
     const bool ck_zero = (g0 >> 16) == 0u; // udp.c:132
-    const uint32_t udp_len = min(ulen, ip_plen); // udp.c:126
+    const uint32_t udp_len = min(ulen, ip_plen); // udp.c:128
     const uint32_t L = udp_len + hl;             // unwrapped; > 65535 is past any frame
 
     uint32_t v;
