@@ -136,8 +136,8 @@ PLANNED = [
     (14, 2048, 1500, "ip", (32, 4, 1)),       # netmap slots, strided
     (14, 2048, 1500, "payload", (32, 3, 2)),
     (0, 1024, 1024, "ip", (32, 4, 2)),
-    (0, 64, 64, "ip", (4, 1, 4)),             # C3 64 B
-    (0, 256, 256, "ip", (8, 3, 2)),
+    (0, 64, 64, "ip", (4, 1, 4)),             # C3 64 B (lean kernel)
+    (0, 256, 256, "ip", (8, 2, 2)),           # lean kernel, the pass filled exactly
     (0, 576, 576, "ip", (16, 3, 1)),
     (0, 9000, 9000, "ip", (32, 18, 1)),
 ]
@@ -145,7 +145,7 @@ PLANNED = [
 
 @pytest.mark.parametrize("base,stride,length,kind,shape", PLANNED)
 def test_planner_shapes(gpu, monkeypatch, base, stride, length, kind, shape):
-    for k in ("WC_SHAPE", "WC_STRIDED_SEG", "WC_VARIANT"):
+    for k in ("WC_SHAPE", "WC_STRIDED_SEG", "WC_VARIANT", "WC_LEAN_MAX"):
         monkeypatch.delenv(k, raising=False)
     wc.reload_config()
     p = wc.plan_strided(0x100000000 + base, stride, length, 1 << 20, kind=kind)
@@ -164,15 +164,19 @@ def test_planner_aligned_small_take_seg(gpu, monkeypatch, length, seg):
     assert (p["group"] == 0) == seg
 
 
-@pytest.mark.parametrize("length,seg", [(64, True), (256, True), (576, True), (992, True),
-                                        (1024, False), (1472, False)])
-def test_planner_payload_packed_take_seg(gpu, monkeypatch, length, seg):
-    """payload_cksum: packed packets below 64 chunks take the seg kernel at any stride."""
-    for k in ("WC_SHAPE", "WC_STRIDED_SEG", "WC_VARIANT"):
+@pytest.mark.parametrize("length,kernel", [(64, "lean"), (128, "lean"), (256, "lean"),
+                                           (576, "seg"), (992, "seg"), (1024, "group"),
+                                           (1472, "group")])
+def test_planner_payload_packed(gpu, monkeypatch, length, kernel):
+    """payload_cksum, packed: aligned packets whose chunk count a lean group
+    pass fills exactly take the lean kernel; the rest below 64 chunks the
+    seg kernel; longer ones the group kernel."""
+    for k in ("WC_SHAPE", "WC_STRIDED_SEG", "WC_VARIANT", "WC_LEAN_MAX"):
         monkeypatch.delenv(k, raising=False)
     wc.reload_config()
     p = wc.plan_strided(0x100000000, length, length, 1 << 20, kind="payload")
-    assert (p["group"] == 0) == seg
+    assert p["kernel"] == kernel
+    assert (p["group"] == 0) == (kernel == "seg")
 
 
 def test_capped_grid_overlapping_stride(gpu):

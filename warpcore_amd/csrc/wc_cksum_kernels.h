@@ -77,30 +77,36 @@
 // wc_k_lean.hip): the planner's FULL shapes up to 576 B plus tuning
 // neighbours for small packets.
 #define WC_LEAN_SHAPE_LIST                                                     \
-    WC_SHAPE(4, 1, 2)                                                          \
-    WC_SHAPE(4, 1, 4)                                                          \
-    WC_SHAPE(4, 2, 2)                                                          \
-    WC_SHAPE(4, 2, 4)                                                          \
-    WC_SHAPE(8, 1, 2)                                                          \
-    WC_SHAPE(8, 1, 4)                                                          \
-    WC_SHAPE(8, 1, 8)                                                          \
-    WC_SHAPE(8, 2, 2)                                                          \
-    WC_SHAPE(8, 2, 4)                                                          \
-    WC_SHAPE(8, 3, 2)                                                          \
-    WC_SHAPE(8, 6, 1)                                                          \
-    WC_SHAPE(16, 1, 4)                                                         \
-    WC_SHAPE(16, 2, 2)                                                         \
-    WC_SHAPE(16, 2, 4)                                                         \
-    WC_SHAPE(16, 3, 1)                                                         \
-    WC_SHAPE(16, 3, 2)                                                         \
-    WC_SHAPE(16, 6, 2)                                                         \
-    WC_SHAPE(32, 2, 2)                                                         \
-    WC_SHAPE(32, 2, 4)                                                         \
-    WC_SHAPE(32, 3, 1)                                                         \
-    WC_SHAPE(32, 3, 2)                                                         \
-    WC_SHAPE(32, 4, 1)                                                         \
-    WC_SHAPE(32, 4, 2)                                                         \
-    WC_SHAPE(32, 18, 1)                                                        \
+    WC_SHAPE(4, 1, 2)                                                      \
+    WC_SHAPE(4, 1, 4)                                                      \
+    WC_SHAPE(4, 2, 2)                                                      \
+    WC_SHAPE(4, 2, 4)                                                      \
+    WC_SHAPE(4, 3, 1)                                                      \
+    WC_SHAPE(8, 1, 2)                                                      \
+    WC_SHAPE(8, 1, 4)                                                      \
+    WC_SHAPE(8, 1, 8)                                                      \
+    WC_SHAPE(8, 2, 2)                                                      \
+    WC_SHAPE(8, 2, 4)                                                      \
+    WC_SHAPE(8, 3, 1)                                                      \
+    WC_SHAPE(8, 3, 2)                                                      \
+    WC_SHAPE(8, 6, 1)                                                      \
+    WC_SHAPE(16, 1, 4)                                                     \
+    WC_SHAPE(16, 2, 2)                                                     \
+    WC_SHAPE(16, 2, 4)                                                     \
+    WC_SHAPE(16, 3, 1)                                                     \
+    WC_SHAPE(16, 3, 2)                                                     \
+    WC_SHAPE(16, 6, 2)                                                     \
+    WC_SHAPE(32, 1, 4)                                                     \
+    WC_SHAPE(32, 2, 2)                                                     \
+    WC_SHAPE(32, 2, 4)                                                     \
+    WC_SHAPE(32, 3, 1)                                                     \
+    WC_SHAPE(32, 3, 2)                                                     \
+    WC_SHAPE(32, 4, 1)                                                     \
+    WC_SHAPE(32, 4, 2)                                                     \
+    WC_SHAPE(32, 18, 1)                                                    \
+    WC_SHAPE(64, 1, 4)                                                     \
+    WC_SHAPE(64, 2, 2)                                                     \
+    WC_SHAPE(64, 3, 1)                                                     \
     WC_SHAPE(64, 4, 1)
 
 namespace wc {

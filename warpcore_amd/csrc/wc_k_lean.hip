@@ -15,11 +15,11 @@
 // those terms do not cover (IPv4 with options or IHL < 5) is recomputed
 // exactly by the lane that stores its result (lane_payload_exact).
 //
-// What makes it lean: the wave's first packet address is scalar (SGPRs), each
-// lane's chunk is a 32-bit offset from it (global_load ... saddr), so the
-// prologue before the first load is a handful of instructions; 4 v_dot2 per
-// chunk instead of 8 v_dot4 byte-lane sums; no masks unless the tail wave or
-// a pass the packet does not fill needs them.  Tiny packets are the case it
+// What makes it lean: the wave's first packet address is scalar (SGPRs) and
+// each lane's chunk a 32-bit offset from it, so the prologue before the
+// first load is mostly scalar; 4 v_dot2 per chunk instead of 8 v_dot4
+// byte-lane sums; no masks unless the tail wave or a pass the packet does
+// not fill needs them (the planner picks shapes the packet fills).  Tiny packets are the case it
 // is for: C3 64 B spends most of a wave's life before its first load and
 // after its last (profiles/ab_r02_lane_store.log).
 #include "wc_seg.h"
@@ -92,15 +92,20 @@ k_cksum_lean(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len, ui
                     d[u][c] = load_at<NT>(gb, lo + (uint32_t)u * ustep + 16u * G * c);
         } else {
             // The tail wave, or a pass the packets do not fill: a dead slot
-            // re-reads the wave's first chunk (inside the batch) and is zeroed.
+            // re-reads another chunk of its own packet (the wave's first
+            // packet past the batch end) and is zeroed -- spread over the
+            // packets' lines, not one hot line for every dead lane.
 #pragma unroll
             for (int u = 0; u < U; ++u)
 #pragma unroll
                 for (int c = 0; c < CPL; ++c) {
-                    const bool live =
-                        p0 + (uint64_t)u * GPW + grp < n && gl + (uint32_t)c * G < nch;
-                    const u32x4 x =
-                        load_at<NT>(gb, live ? lo + (uint32_t)u * ustep + 16u * G * c : 0u);
+                    const uint32_t k = gl + (uint32_t)c * G;
+                    const bool pv = p0 + (uint64_t)u * GPW + grp < n;
+                    const bool live = pv && k < nch;
+                    const uint32_t kk = k < nch ? k : (k - nch < nch ? k - nch : 0u);
+                    const uint32_t off =
+                        pv ? grp * (uint32_t)stride + (uint32_t)u * ustep + 16u * kk : 16u * kk;
+                    const u32x4 x = load_at<NT>(gb, off);
                     d[u][c] = live ? x : u32x4{0u, 0u, 0u, 0u};
                 }
         }
