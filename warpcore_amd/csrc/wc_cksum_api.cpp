@@ -335,20 +335,23 @@ wc::Shape shape_for_chunks(uint32_t nch, bool full, bool payload, bool aligned)
 
 // Lean-kernel shape: a group whose one pass the packet fills exactly (G *
 // CPL == chunks, no dead slots -- a pass the packet does not fill costs the
-// masked path, measured 70 vs 91 % at 576 B: profiles/ab_r03_lean.log),
-// with ~4 loads in flight per lane; {0,0,0} when no such shape exists
-// (packets under 4 chunks take the masked path of (4, 1, 4)).
+// masked path: 576 B in (16,3,1) ran at 70 vs 91 %), groups of >= 8 lanes
+// (a 4-lane group reads 64-B half lines per load, 128 B in (4,2,2) ran at
+// 75 vs 89 % in (8,1,4)) except for 64-B packets, which 4-lane groups read
+// as one contiguous kilobyte per load; ~4 loads in flight per lane
+// (profiles/ab_r03_lean*.log).  {0,0,0}: no such shape, not lean.  Packets
+// under 4 chunks take the masked path of (4, 1, 4).
 wc::Shape lean_shape_for(uint32_t nch)
 {
     if (nch <= 4)
         return {4, 1, 4};
-    for (int g = 4; g <= 64; g *= 2) {
+    for (int g = 8; g <= 64; g *= 2) {
         if (nch % (uint32_t)g)
             continue;
         const int cpl = (int)(nch / (uint32_t)g);
         if (cpl > 3)
             continue;
-        return {g, cpl, cpl == 1 ? 4 : cpl == 2 ? 2 : 1};
+        return {g, cpl, cpl == 1 ? 4 : cpl == 2 ? 2 : (g <= 8 ? 2 : 1)};
     }
     return {0, 0, 0};
 }
