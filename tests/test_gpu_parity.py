@@ -1018,8 +1018,11 @@ def test_lean_kernel_aligned(gpu, monkeypatch, length, shape):
             for i in range(n):
                 o = i * stride
                 r = i % 5
-                if r == 4:
-                    continue  # random bytes as the header
+                if r == 4:  # random bytes as the header, IHL kept within len
+                    b0 = int(hb[o])
+                    if b0 >> 4 == 4 and (b0 & 15) * 4 > length:
+                        hb[o] = 0x40 | (length // 4 & 15)
+                    continue
                 pl = rng.integers(0, 256, max(0, length - 48), dtype=np.uint8).tobytes()
                 if r == 0:
                     pkt, _ = ipv6_udp(pl + bytes(max(0, 48 - 48)), rng)

@@ -9,7 +9,10 @@ export TMPDIR=/tmp WC_NO_BUILD=1
 T="timeout -k 10 120 python tools/tune.py --rounds ${ROUNDS:-4} --iters 20"
 for c in ${CASES:-c4:payload}; do
     cfg=${c%%:*}; kind=${c##*:}; hdr=""
-    case $kind in payload+h) kind=payload; hdr="--headers" ;; esac
+    case $kind in
+        payload+h) kind=payload; hdr="--headers" ;;
+        fused) kind=payload; hdr="--headers --fused" ;;
+    esac
     case $cfg in
         c2) a="--config c2" ;;
         c4) a="--config c4" ;;

@@ -76,9 +76,9 @@ __device__ __forceinline__ RxParse rx_parse(uint64_t fa, uint32_t flen, bool val
     const uint64_t a1 = fa + 12u;
     const Win2 w1 = win2_load(a1, fend, valid && flen > 12u, zero);
     const uint32_t s1 = (uint32_t)(a1 & 15u);
-    const uint32_t f0 = win_bytes(w1.x, w1.y, w1.y, s1, 0); // frame 12..15
-    const uint32_t f1 = win_bytes(w1.x, w1.y, w1.y, s1, 1); // frame 16..19 = ip 2..5
-    const uint32_t f2 = win_bytes(w1.x, w1.y, w1.y, s1, 2); // frame 20..23 = ip 6..9
+    uint32_t fw[3]; // frame 12..15, 16..19 = ip 2..5, 20..23 = ip 6..9
+    win_rot(w1.x, w1.y, w1.y, s1, fw);
+    const uint32_t f0 = fw[0], f1 = fw[1], f2 = fw[2];
     const uint32_t etype = ((f0 & 0xFFu) << 8) | ((f0 >> 8) & 0xFFu); // eth.h:44-53
     const uint32_t b0 = (f0 >> 16) & 0xFFu;                              // vhl / vfc
     const bool v4 = etype == 0x0800u, v6 = etype == 0x86DDu;
@@ -166,12 +166,14 @@ k_rx_verdict(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
     struct Lds {
         FlatLds<UNS> f; // slot table, row marks, prefix sums
         u32x4 stage[64 * UNS];
+        u32x4 pm[17]; // seg_head's masks
     };
     __shared__ Lds lds_all[kFlatWaves];
 
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
     Lds &L = lds_all[w];
+    seg_init_masks(L.pm, lane); // read after the first row group's wave_order
     const uint64_t ntiles = (n + 63) / 64;
     const uint64_t nwaves = (uint64_t)gridDim.x * kFlatWaves;
     uint64_t tile = xcd_block(13 << 8) * kFlatWaves + w; // the seg kernel's XCD span
@@ -199,7 +201,7 @@ k_rx_verdict(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
             bool done = true;
             uint16_t rh = 0;
             uint16_t r = seg_tile<UNS, WC_KIND_PAYLOAD, NT, false, GathSrc<UNS, NT>, true>(
-                L.f.pre, L.stage, lane, h.ip, 16ull * t.cp + (h.ip & 15u), h.plen, h.need,
+                L.f.pre, L.stage, L.pm, lane, h.ip, 16ull * t.cp + (h.ip & 15u), h.plen, h.need,
                 t.total, GathSrc<UNS, NT>{&L.f, t}, zero, done, rh);
             if (h.need && !done) // header longer than the packet, or a possible wrap
                 r = lane_payload_exact<NT>(h.ip, h.plen);

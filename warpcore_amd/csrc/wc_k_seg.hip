@@ -51,10 +51,13 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     };
     using TileLds = typename std::conditional<kSegOnly, SegOnlyLds, FullLds>::type;
     __shared__ TileLds lds_all[kFlatWaves];
+    __shared__ u32x4 head_masks[kFlatWaves][17]; // seg_head's tables, one per wave
 
     const int lane = threadIdx.x & 63;
     const int w = threadIdx.x >> 6;
     TileLds &L = lds_all[w];
+    const u32x4 *pm = head_masks[w];
+    seg_init_masks(head_masks[w], lane); // read after the first row group's wave_order
     const uint64_t ntiles = (n + 63) / 64;
     const uint64_t nwaves = (uint64_t)gridDim.x * kFlatWaves;
     // XCD super-blocks of 2^13 workgroups (32768 tiles) unless WC_VARIANT
@@ -130,7 +133,7 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
         uint16_t rh = 0;
         if constexpr (kSegOnly) {
             r = seg_tile<UNS, KIND, NT, HDR, DenseSrc<UNS, NT>, true>(
-                L.seg.pre, L.seg.stage, lane, a, a - A0, len, valid, T,
+                L.seg.pre, L.seg.stage, pm, lane, a, a - A0, len, valid, T,
                 DenseSrc<UNS, NT>{A0, T, zero}, zero, done, rh);
             if constexpr (KIND == WC_KIND_PAYLOAD)
                 if (!done)
@@ -139,7 +142,7 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
         else if (!HDR && grouped)
             r = grp_tile<UNG, KIND, NT, HDR>(L.grp, lane, a, len, valid, Rq, zero, done, rh);
         else if (dense)
-            r = seg_tile<UNS, KIND, NT, HDR>(L.seg.pre, L.seg.stage, lane, a, a - A0, len, valid,
+            r = seg_tile<UNS, KIND, NT, HDR>(L.seg.pre, L.seg.stage, pm, lane, a, a - A0, len, valid,
                                              T, DenseSrc<UNS, NT>{A0, T, zero}, zero, done, rh);
         else if (!STR && gather) {
             // Gathered stream: the tile's packets' chunks in packet order
@@ -147,7 +150,7 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
             const uint32_t span = KIND == WC_KIND_PAYLOAD ? max(len, 20u) : len;
             const FlatTile t = flat_tile_setup<UNS, 1>(L.gat.f, lane, a, len, span, valid, 0u);
             if (t.total != 0)
-                r = seg_tile<UNS, KIND, NT, HDR>(L.gat.f.pre, L.gat.stage, lane, a,
+                r = seg_tile<UNS, KIND, NT, HDR>(L.gat.f.pre, L.gat.stage, pm, lane, a,
                                                  16ull * t.cp + (a & 15u), len, valid, t.total,
                                                  GathSrc<UNS, NT>{&L.gat.f, t}, zero, done, rh);
             wave_order(); // the flat path below rewrites the tables

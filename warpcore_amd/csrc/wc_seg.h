@@ -183,6 +183,55 @@ __device__ __forceinline__ uint32_t win_bytes(const u32x4 &x, const u32x4 &y, co
                                      8u * (s & 3u));
 }
 
+// Packet bytes 4 m .. 4 m + 3 for m = 0 .. W - 1 from the window x:y:z that
+// holds the packet's first bytes from offset s (< 16) on: the window is
+// rotated by s >> 2 dwords in two select levels, then each output dword is
+// one alignbit -- about 3 W + 4 VALU for all W, where W separate win_bytes
+// calls select each dword out of 12 (about 14 VALU apiece).
+template <int W>
+__device__ __forceinline__ void win_rot(const u32x4 &x, const u32x4 &y, const u32x4 &z,
+                                        uint32_t s, uint32_t (&w)[W])
+{
+    static_assert(W >= 1 && W <= 5, "window of 48 bytes from offset < 16");
+    // Named scalars, not an array: a select between two array elements is
+    // turned into a dynamic index, which puts the array in scratch.
+    const bool q1 = s & 4u, q2 = s & 8u;
+    const uint32_t e0 = q1 ? x.y : x.x, e1 = q1 ? x.z : x.y, e2 = q1 ? x.w : x.z,
+                   e3 = q1 ? y.x : x.w, e4 = q1 ? y.y : y.x, e5 = q1 ? y.z : y.y,
+                   e6 = q1 ? y.w : y.z, e7 = q1 ? z.x : y.w, e8 = q1 ? z.y : z.x;
+    const uint32_t d0 = q2 ? e2 : e0, d1 = q2 ? e3 : e1, d2 = q2 ? e4 : e2, d3 = q2 ? e5 : e3,
+                   d4 = q2 ? e6 : e4, d5 = q2 ? e7 : e5;
+    (void)e8;
+    const uint32_t sh = 8u * (s & 3u);
+    w[0] = __builtin_amdgcn_alignbit(d1, d0, sh);
+    if constexpr (W > 1)
+        w[1] = __builtin_amdgcn_alignbit(d2, d1, sh);
+    if constexpr (W > 2)
+        w[2] = __builtin_amdgcn_alignbit(d3, d2, sh);
+    if constexpr (W > 3)
+        w[3] = __builtin_amdgcn_alignbit(d4, d3, sh);
+    if constexpr (W > 4)
+        w[4] = __builtin_amdgcn_alignbit(d5, d4, sh);
+}
+
+// V of a chunk's first q bytes (q <= 16) with the head masks from LDS: one
+// 16-byte LDS read and 4 v_and, where head_mask computes each dword's mask
+// in ~5 VALU.  pm[k] = 0xFF in bytes [0, k) (seg_init_masks).
+__device__ __forceinline__ uint32_t seg_head(const u32x4 &d, uint32_t q, const u32x4 *pm)
+{
+    const u32x4 m = pm[q];
+    return wsum(d.w & m.w, wsum(d.z & m.z, wsum(d.y & m.y, wsum(d.x & m.x, 0u))));
+}
+
+// Fill the 17 head masks (lanes 0..16 of the calling wave).
+__device__ __forceinline__ void seg_init_masks(u32x4 *pm, int lane)
+{
+    if (lane < 17) {
+        const uint32_t k = (uint32_t)lane;
+        pm[k] = u32x4{head_mask(k, 0), head_mask(k, 1), head_mask(k, 2), head_mask(k, 3)};
+    }
+}
+
 // Could the reference's uint32 sum for this odd-start payload packet wrap
 // when `special` is added?  Before it, the sum holds at most (len + 1) / 2 + 1
 // words of <= 0xFFFF (body, src/dst and proto or payload length; len >= hl),
@@ -248,10 +297,10 @@ struct GathSrc {
 // their result, and the caller recomputes that lane's packet exactly
 // (lane_payload_exact) -- no flat path in that kernel.
 template <int UNS, int KIND, bool NT, bool HDR, class Src, bool LANEFIX = false>
-__device__ __forceinline__ uint16_t seg_tile(uint32_t *pre, u32x4 *stage, int lane, uint64_t a,
-                                             uint64_t ra, uint32_t len, bool valid, uint32_t T,
-                                             const Src &src, uint64_t zero, bool &done,
-                                             uint16_t &rh)
+__device__ __forceinline__ uint16_t seg_tile(uint32_t *pre, u32x4 *stage, const u32x4 *pm,
+                                             int lane, uint64_t a, uint64_t ra, uint32_t len,
+                                             bool valid, uint32_t T, const Src &src,
+                                             uint64_t zero, bool &done, uint16_t &rh)
 {
     constexpr uint32_t kGrp = 64u * UNS;
     constexpr bool PL = KIND == WC_KIND_PAYLOAD;
@@ -304,7 +353,7 @@ __device__ __forceinline__ uint16_t seg_tile(uint32_t *pre, u32x4 *stage, int la
         Pe = carry;
     done = true;
     if constexpr (!PL) {
-        const uint32_t v = (Pe + seg_chunk<true>(he, qe)) - (Ps + seg_chunk<true>(hs, qs));
+        const uint32_t v = (Pe + seg_head(he, qe, pm)) - (Ps + seg_head(hs, qs, pm));
         if (!(a & 1u))
             return fold_not(v);
         return fold_not(__builtin_amdgcn_alignbit(v, v, 24)); // rotl32(v, 8)
@@ -312,8 +361,9 @@ __device__ __forceinline__ uint16_t seg_tile(uint32_t *pre, u32x4 *stage, int la
         // Header bytes 0..11 from the packet's first two chunks (hs = c0, h1 =
         // c0 + 1); the start chunk cs is one of them.
         const uint32_t s = (uint32_t)(a & 15u);
-        const uint32_t w0 = win_bytes(hs, h1, h2, s, 0), w1 = win_bytes(hs, h1, h2, s, 1),
-                       w2 = win_bytes(hs, h1, h2, s, 2);
+        uint32_t wv[HDR ? 5 : 3]; // packet bytes 0..11 (0..19 with the header checksum)
+        win_rot(hs, h1, h2, s, wv);
+        const uint32_t w0 = wv[0], w1 = wv[1], w2 = wv[2];
         const PseudoHdr ph = pseudo_hdr(w0 & 0xFFu, (w0 >> 16) & 0xFFu, w0 >> 24,
                                         (w1 >> 16) & 0xFFu);
         const bool lane_bad = valid && !seg_payload_ok(a, len, ph);
@@ -326,7 +376,7 @@ __device__ __forceinline__ uint16_t seg_tile(uint32_t *pre, u32x4 *stage, int la
         const u32x4 hq = cs == c0 ? hs : h1;
         // V of [a + 8, a + len): IPv6 src/dst + body (hl = 40); IPv4 bytes
         // 8..11, src/dst, options, body.
-        uint32_t v = (Pe + seg_chunk<true>(he, qe)) - (Ps + seg_chunk<true>(hq, qs));
+        uint32_t v = (Pe + seg_head(he, qe, pm)) - (Ps + seg_head(hq, qs, pm));
         const uint32_t odd = (uint32_t)(a & 1u);
         if (ph.v4) {
             // Minus bytes 8..11 (ttl, proto, header checksum), plus proto << 8
@@ -364,7 +414,7 @@ __device__ __forceinline__ uint16_t seg_tile(uint32_t *pre, u32x4 *stage, int la
             // dword's bytes at their address weight, as wsum of the dword,
             // byte-swapped per word for an odd start), then minus the bytes
             // [hl, 20) or plus [20, hl) summed above.  Folded like ip_cksum.
-            const uint32_t w3 = win_bytes(hs, h1, h2, s, 3), w4 = win_bytes(hs, h1, h2, s, 4);
+            const uint32_t w3 = wv[HDR ? 3 : 0], w4 = wv[HDR ? 4 : 0];
             const uint32_t sw = odd ? 0x02030001u : 0x03020100u;
             uint32_t vh = wsum(__builtin_amdgcn_perm(w0, w0, sw), 0u);
             vh = wsum(__builtin_amdgcn_perm(w1, w1, sw), vh);
