@@ -112,7 +112,15 @@ k_cksum_lean(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len, ui
         if constexpr (CPL * U < 16)
             __builtin_amdgcn_sched_barrier(0); // every load before the first sum
 
-        uint32_t res = 0;
+        // Per packet-round u: the group's word sum, handed to lane j = its
+        // packet's store lane (packet p0 + j) together with, for
+        // payload_cksum, the packet's first 12 bytes from the group leader.
+        // The per-packet terms and the fold then run once per wave-iteration
+        // for all 64 packets, not once per round (64-B payload_cksum 10.5 ->
+        // 10.0-10.1 us, ip_cksum 9.8-10.0 -> 9.7 us in tune.py A/B,
+        // profiles/ab_r03_lean_xpose.log).
+        uint32_t Vs = 0, hx = 0, hy = 0, hz = 0;
+        const int src = (lane % GPW) * G;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             uint32_t V = 0;
@@ -123,20 +131,26 @@ k_cksum_lean(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len, ui
                 else
                     V = wsum4(d[u][c], V);
             }
-            uint32_t flag = 0;
-            if constexpr (PL) {
-                bool ok = true;
-                const uint32_t extra = lean_extra(d[u][0], ok);
-                V += gl == 0 ? extra : 0u;
-                flag = ok ? 0u : 0x10000u;
-            }
             V = group_sum<G>(V);
-            // Lane j of the wave takes packet p0 + j's result from its group
-            // leader (the leader's header flag rides in bit 16).
-            const int src = (lane % GPW) * G;
-            const uint32_t r = __shfl((uint32_t)fold_not(V) | flag, src, 64);
-            if (lane / GPW == u)
-                res = r;
+            const bool mine = lane / GPW == u;
+            const uint32_t v = __shfl(V, src, 64);
+            Vs = mine ? v : Vs;
+            if constexpr (PL) {
+                const uint32_t x = __shfl(d[u][0].x, src, 64);
+                const uint32_t y = __shfl(d[u][0].y, src, 64);
+                const uint32_t z = __shfl(d[u][0].z, src, 64);
+                hx = mine ? x : hx;
+                hy = mine ? y : hy;
+                hz = mine ? z : hz;
+            }
+        }
+        uint32_t res;
+        if constexpr (PL) {
+            bool ok = true;
+            Vs += lean_extra(u32x4{hx, hy, hz, 0u}, ok);
+            res = (uint32_t)fold_not(Vs) | (ok ? 0u : 0x10000u);
+        } else {
+            res = fold_not(Vs);
         }
         const uint64_t i = p0 + (uint64_t)lane;
         if (lane < (int)PPW && i < n) {
