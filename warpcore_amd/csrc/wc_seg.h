@@ -107,7 +107,7 @@ __device__ __forceinline__ void seg_issue(SegRows<UNS> &R, uint64_t A0, uint32_t
 template <int UNS, int HC, bool CLAMP>
 __device__ __forceinline__ void seg_accum(const SegRows<UNS> &R, uint32_t *pre, u32x4 *stage,
                                           uint32_t g0, int lane, uint32_t T, uint32_t cs,
-                                          uint32_t ce, uint32_t c0, uint32_t &carry,
+                                          uint32_t ce, uint32_t c0, uint32_t sa, uint32_t &carry,
                                           uint32_t &Ps, uint32_t &Pe, u32x4 &hs, u32x4 &he,
                                           u32x4 &h1, u32x4 &h2)
 {
@@ -141,13 +141,18 @@ __device__ __forceinline__ void seg_accum(const SegRows<UNS> &R, uint32_t *pre, 
     // The packet's first / last chunk, for its partial sums (exec-masked
     // LDS reads: no scattered global re-loads).
     if constexpr (HC >= 2) {
+        // Header chunks c0 .. c0 + 2: bytes 0..11 (0..19 with the header
+        // checksum) from the packet's start phase sa on -- the second chunk
+        // only if sa > 4 (with the checksum: always), the third only if
+        // sa > 12 (fewer LDS reads and bank conflicts than every lane
+        // reading all three).
         const uint32_t d0 = c0 - g0; // (unsigned: c0 + 1 == g0 gives d0 + 1 == 0)
         if (d0 < kGrp)
             hs = stage[d0];
-        if (d0 + 1u < kGrp)
+        if ((HC >= 3 || sa > 4u) && d0 + 1u < kGrp)
             h1 = stage[d0 + 1u];
         if constexpr (HC >= 3)
-            if (d0 + 2u < kGrp)
+            if (sa > 12u && d0 + 2u < kGrp)
                 h2 = stage[d0 + 2u];
     } else {
         if (ds < kGrp)
@@ -310,6 +315,7 @@ __device__ __forceinline__ uint16_t seg_tile(uint32_t *pre, u32x4 *stage, const 
     const uint32_t cs = (uint32_t)(rs >> 4), qs = (uint32_t)(rs & 15u);
     const uint32_t ce = (uint32_t)(re >> 4), qe = (uint32_t)(re & 15u);
     const uint32_t c0 = (uint32_t)(ra >> 4);
+    const uint32_t sa = (uint32_t)(ra & 15u); // == a & 15 (dense and gathered streams)
 
     SegRows<UNS> A, B;
     src.issue(A, 0, lane);
@@ -324,7 +330,7 @@ __device__ __forceinline__ uint16_t seg_tile(uint32_t *pre, u32x4 *stage, const 
     // 20 rows instead of 24).
     uint32_t j = 0;
 #define WC_SEG_ACC(R, G)                                                       \
-    seg_accum<UNS, HC, CL>(R, pre, stage, G, lane, T, cs, ce, c0, carry, Ps, Pe, hs, he, h1, h2)
+    seg_accum<UNS, HC, CL>(R, pre, stage, G, lane, T, cs, ce, c0, sa, carry, Ps, Pe, hs, he, h1, h2)
     for (; j + 2 * kGrp < T; j += 2 * kGrp) {
         src.issue(B, j + kGrp, lane);
         __builtin_amdgcn_sched_barrier(0);
