@@ -15,7 +15,10 @@ fi
 T="timeout -k 10 200 python tools/tune.py --rounds ${ROUNDS:-6} --iters 20"
 for c in ${CASES:-c2:ip c2:payload}; do
     cfg=${c%%:*}; kind=${c##*:}; hdr=""
-    case $kind in payload+h) kind=payload; hdr="--headers" ;; esac
+    case $kind in
+        payload+h) kind=payload; hdr="--headers" ;;
+        fused) kind=payload; hdr="--headers --fused" ;;
+    esac
     case $cfg in
         c2) a="--config c2" ;;
         c4) a="--config c4" ;;

@@ -52,9 +52,10 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     using TileLds = typename std::conditional<kSegOnly, SegOnlyLds, FullLds>::type;
     __shared__ TileLds lds_all[kFlatWaves];
     __shared__ u32x4 head_masks[kFlatWaves][17]; // seg_head's tables, one per wave
+    __shared__ u32x4 res_stage[kFlatWaves][HDR ? 16 : 8]; // the tile's results (tile_store_wide)
 
     const int lane = threadIdx.x & 63;
-    const int w = threadIdx.x >> 6;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); // wave-uniform: SGPR
     TileLds &L = lds_all[w];
     const u32x4 *pm = head_masks[w];
     seg_init_masks(head_masks[w], lane); // read after the first row group's wave_order
@@ -175,11 +176,14 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
             if constexpr (HDR)
                 rh = valid && ph.v4 ? lane_hdr_cksum<NT>(a, ph.hl, nullptr) : (uint16_t)0;
         }
+        // Results: 16-byte stores from a few lanes (tile_store_wide).
+        const bool per_lane = variant & (1 << 26); // (tuning: the per-lane 2-byte stores)
         if constexpr (HDR)
-            if (valid)
-                out_hdr[p] = rh;
-        if (valid && out)
-            out[p] = r;
+            tile_store_wide<2>(res_stage[w], lane, r, rh, out, out_hdr, tile, nvalid, per_lane,
+                               (variant >> 28) & 7);
+        else if (out)
+            tile_store_wide<1>(res_stage[w], lane, r, 0, out, nullptr, tile, nvalid, per_lane,
+                               (variant >> 28) & 7);
         nbad += valid && r != 0;
         wave_order(); // the tables are rewritten by the next tile
     }
@@ -196,8 +200,12 @@ static hipError_t launch_seg_kernel(const LaunchArgs &a, hipStream_t st)
 {
     constexpr int UN = 2;
     const uint64_t tiles = (a.n + 63) / 64;
-    const int grid = (int)std::min<uint64_t>(
+    int grid = (int)std::min<uint64_t>(
         kMaxGridBlocks, std::max<uint64_t>(1, (tiles + kFlatWaves - 1) / kFlatWaves));
+#ifdef WC_TUNING
+    if ((a.variant >> 20) & 15) // A/B: cap the grid at k * 1024 blocks (several tiles per wave)
+        grid = std::min(grid, ((a.variant >> 20) & 15) * 1024);
+#endif
     const uint8_t *b = (const uint8_t *)a.base;
     unsigned long long *bad = (unsigned long long *)a.bad;
     if (a.out_hdr) {
