@@ -20,7 +20,7 @@ k_cksum_flat(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
     __syncthreads();
 
     const int lane = threadIdx.x & 63;
-    const int w = threadIdx.x >> 6;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); // wave-uniform: SGPR
     FlatLds<UN> &L = lds_all[w];
     const uint64_t ntiles = (n + 63) / 64;
     const uint64_t nwaves = (uint64_t)gridDim.x * kFlatWaves;

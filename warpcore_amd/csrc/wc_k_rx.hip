@@ -171,7 +171,7 @@ k_rx_verdict(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
     __shared__ Lds lds_all[kFlatWaves];
 
     const int lane = threadIdx.x & 63;
-    const int w = threadIdx.x >> 6;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); // wave-uniform: SGPR
     Lds &L = lds_all[w];
     seg_init_masks(L.pm, lane); // read after the first row group's wave_order
     const uint64_t ntiles = (n + 63) / 64;

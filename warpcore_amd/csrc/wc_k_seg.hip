@@ -52,7 +52,6 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     using TileLds = typename std::conditional<kSegOnly, SegOnlyLds, FullLds>::type;
     __shared__ TileLds lds_all[kFlatWaves];
     __shared__ u32x4 head_masks[kFlatWaves][17]; // seg_head's tables, one per wave
-    __shared__ u32x4 res_stage[kFlatWaves][HDR ? 16 : 8]; // the tile's results (tile_store_wide)
 
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); // wave-uniform: SGPR
@@ -176,14 +175,18 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
             if constexpr (HDR)
                 rh = valid && ph.v4 ? lane_hdr_cksum<NT>(a, ph.hl, nullptr) : (uint16_t)0;
         }
-        // Results: 16-byte stores from a few lanes (tile_store_wide).
-        const bool per_lane = variant & (1 << 26); // (tuning: the per-lane 2-byte stores)
-        if constexpr (HDR)
-            tile_store_wide<2>(res_stage[w], lane, r, rh, out, out_hdr, tile, nvalid, per_lane,
-                               (variant >> 28) & 7);
-        else if (out)
-            tile_store_wide<1>(res_stage[w], lane, r, 0, out, nullptr, tile, nvalid, per_lane,
-                               (variant >> 28) & 7);
+        // Both results from one block, after every path's loads: apart, hipcc
+        // put an s_waitcnt vmcnt(0) between the two stores, so the second
+        // waited for the first one's write (C4 fused 649 -> 641 us).  The
+        // results' HBM writes themselves cost C4 ~30 us per 32 MB array
+        // whatever their form -- 16-byte chunks, one 512-B run per block of
+        // tiles, nt / sc1 (profiles/ab_r03_fused_store.log).
+        if (valid) {
+            if constexpr (HDR)
+                out_hdr[p] = rh;
+            if (out)
+                out[p] = r;
+        }
         nbad += valid && r != 0;
         wave_order(); // the tables are rewritten by the next tile
     }

@@ -237,49 +237,6 @@ __device__ __forceinline__ void seg_init_masks(u32x4 *pm, int lane)
     }
 }
 
-// A tile's 64 results (and, with NARR = 2, its 64 fused header checksums)
-// stored as 16-byte chunks by 8 (16) lanes, staged through LDS.  One 2-byte
-// store per lane cost C4 ~30 us per 32 MB of results (4.5-5 % of the kernel:
-// 64 narrow lane writes per wave-instruction instead of 8 wide ones), where
-// the same bytes as dwordx4 cost a few us (profiles/ab_r03_fused_store.log).
-// A partial tile or an output that is not 16-byte aligned keeps the per-lane
-// stores.  `st` is the wave's LDS staging (8 * NARR chunks).
-template <int NARR>
-__device__ __forceinline__ void tile_store_wide(u32x4 *st, int lane, uint16_t r0, uint16_t r1,
-                                                uint16_t *o0, uint16_t *o1, uint64_t tile,
-                                                uint32_t nvalid, bool per_lane = false,
-                                                int pol = 0)
-{
-    const uintptr_t al = (uintptr_t)o0 | (NARR > 1 ? (uintptr_t)o1 : (uintptr_t)0);
-    if (nvalid == 64u && !(al & 15u) && !per_lane) { // wave-uniform
-        uint16_t *s16 = (uint16_t *)st;
-        s16[lane] = r0;
-        if constexpr (NARR > 1)
-            s16[64 + lane] = r1;
-        __asm__ volatile("" ::: "memory"); // 2-byte writes, 16-byte reads of the same LDS
-        wave_order();
-        if (lane < 8 * NARR) {
-            const u32x4 v = st[lane];
-            uint16_t *dst = (NARR > 1 && lane >= 8 ? o1 : o0) + tile * 64u + 8u * (lane & 7);
-            if (pol == 1)
-                __asm__ volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst), "v"(v) : "memory");
-            else if (pol == 2)
-                __asm__ volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(dst), "v"(v) : "memory");
-            else if (pol == 3)
-                __asm__ volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(dst), "v"(v) : "memory");
-            else if (pol == 4)
-                __asm__ volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(dst), "v"(v) : "memory");
-            else
-                *(u32x4 *)dst = v;
-        }
-        wave_order(); // st is rewritten by the next tile
-    } else if ((uint32_t)lane < nvalid) {
-        o0[tile * 64u + lane] = r0;
-        if constexpr (NARR > 1)
-            o1[tile * 64u + lane] = r1;
-    }
-}
-
 // Could the reference's uint32 sum for this odd-start payload packet wrap
 // when `special` is added?  Before it, the sum holds at most (len + 1) / 2 + 1
 // words of <= 0xFFFF (body, src/dst and proto or payload length; len >= hl),
