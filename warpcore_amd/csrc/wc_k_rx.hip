@@ -66,61 +66,47 @@ __device__ __forceinline__ Win2 win2_load(uint64_t at, uint64_t fend, bool on, u
 
 constexpr int kHdrChunks = 5; // an IPv4 header (<= 60 B) at any phase
 
-// Steps 1 and 2 for this lane's frame [fa, fa + flen).  The branch order is
-// the reference's; bytes past the frame only feed decisions that the length
-// checks have already made.
-__device__ __forceinline__ RxParse rx_parse(uint64_t fa, uint32_t flen, bool valid, uint64_t zero)
+// The header view shared by both parses: EtherType, version, IHL, lengths.
+struct RxHdr {
+    bool v4, v6, version_ok, hdr_in, frag, udp_in;
+    uint32_t hl, room, proto, ip_plen;
+};
+
+__device__ __forceinline__ RxHdr rx_hdr(uint32_t f0, uint32_t f1, uint32_t f2, uint32_t flen)
 {
-    RxParse h{fa + 14u, 0u, kRxTruncated, false};
-    const uint64_t fend = fa + flen;
-    const uint64_t a1 = fa + 12u;
-    const Win2 w1 = win2_load(a1, fend, valid && flen > 12u, zero);
-    const uint32_t s1 = (uint32_t)(a1 & 15u);
-    uint32_t fw[3]; // frame 12..15, 16..19 = ip 2..5, 20..23 = ip 6..9
-    win_rot(w1.x, w1.y, w1.y, s1, fw);
-    const uint32_t f0 = fw[0], f1 = fw[1], f2 = fw[2];
+    RxHdr x;
     const uint32_t etype = ((f0 & 0xFFu) << 8) | ((f0 >> 8) & 0xFFu); // eth.h:44-53
     const uint32_t b0 = (f0 >> 16) & 0xFFu;                              // vhl / vfc
-    const bool v4 = etype == 0x0800u, v6 = etype == 0x86DDu;
-    const uint32_t room = flen >= 14u ? flen - 14u : 0u; // IP bytes inside the frame
-    const uint32_t hl = v4 ? (b0 & 15u) * 4u : 40u;      // ip4.h:88-92, udp.c:113
-    const bool version_ok = (b0 >> 4) == (v4 ? 4u : 6u);
+    x.v4 = etype == 0x0800u;
+    x.v6 = etype == 0x86DDu;
+    x.room = flen >= 14u ? flen - 14u : 0u; // IP bytes inside the frame
+    x.hl = x.v4 ? (b0 & 15u) * 4u : 40u;    // ip4.h:88-92, udp.c:113
+    x.version_ok = (b0 >> 4) == (x.v4 ? 4u : 6u);
     // Header fields (ip4.h:55-66, ip6.h:45-57): valid once the header is in.
-    const bool hdr_in = (v4 || v6) && room >= 1u && version_ok && room >= (v4 ? max(hl, 20u) : 40u);
-    const uint32_t proto = v4 ? f2 >> 24 : f2 & 0xFFu; // p @9 / next_hdr @6
+    x.hdr_in = (x.v4 || x.v6) && x.room >= 1u && x.version_ok &&
+               x.room >= (x.v4 ? max(x.hl, 20u) : 40u);
+    x.proto = x.v4 ? f2 >> 24 : f2 & 0xFFu; // p @9 / next_hdr @6
     // IP4_OFFMASK 0xff1f on the native word @6: the fragment offset (ip4.h:49)
-    const bool frag = v4 && (((f2 & 0x1Fu) | (f2 & 0xFF00u)) != 0u);
-    const uint32_t ip_plen =
-        v4 ? ((((f1 & 0xFFu) << 8) | ((f1 >> 8) & 0xFFu)) - hl) & 0xFFFFu // udp.c:104, wraps
-           : (((f1 >> 16) & 0xFFu) << 8) | (f1 >> 24);                     // udp.c:114
-    const bool udp_in = hdr_in && proto == 17u && ip_plen >= 8u && room >= hl + 8u;
+    x.frag = x.v4 && (((f2 & 0x1Fu) | (f2 & 0xFF00u)) != 0u);
+    x.ip_plen = x.v4 ? ((((f1 & 0xFFu) << 8) | ((f1 >> 8) & 0xFFu)) - x.hl) & 0xFFFFu // udp.c:104
+                     : (((f1 >> 16) & 0xFFu) << 8) | (f1 >> 24);                     // udp.c:114
+    x.udp_in = x.hdr_in && x.proto == 17u && x.ip_plen >= 8u && x.room >= x.hl + 8u;
+    return x;
+}
 
-    // Step 2: the UDP length / checksum fields (udp.h:41-46) at ip + hl + 4,
-    // and the IPv4 header's chunks, all issued before any is used.
-    const uint64_t a2 = h.ip + hl + 4u;
-    const Win2 w2 = win2_load(a2, fend, valid && udp_in, zero);
-    const bool hsum = valid && hdr_in && v4;
-    const uint32_t sip = (uint32_t)(h.ip & 15u);
-    const uint64_t cip = h.ip & ~15ull;
-    const uint32_t nh = hsum ? (sip + hl + 15u) >> 4 : 0u;
-    u32x4 hc[kHdrChunks];
-#pragma unroll
-    for (int k = 0; k < kHdrChunks; ++k)
-        hc[k] = load_chunk<false>((uint32_t)k < nh ? cip + 16ull * k : zero);
-    // ip_cksum(ip, hl) (ip4.c:110-115): word sum at even addresses; an odd
-    // start folds rotl32(V, 8) (the seg path's residue identity; <= 30 words,
-    // no wrap).
-    uint32_t V = 0;
-#pragma unroll
-    for (int k = 0; k < kHdrChunks; ++k)
-        V += seg_range(hc[k], 16 * k - (int)sip, 0, (int)hl);
-    const uint16_t ipck = fold_not((h.ip & 1u) ? __builtin_amdgcn_alignbit(V, V, 24) : V);
-    const uint32_t g0 = win_bytes(w2.x, w2.y, w2.y, (uint32_t)(a2 & 15u), 0);
+// The reference's decision chain (eth_rx -> ip4_rx / ip6_rx -> udp_rx); bytes
+// past the frame only feed decisions that the length checks have made.
+__device__ __forceinline__ RxParse rx_decide(uint64_t fa, uint32_t flen, bool valid,
+                                             const RxHdr &x, uint32_t g0, uint16_t ipck)
+{
+    RxParse h{fa + 14u, 0u, kRxTruncated, false};
+    const bool v4 = x.v4, v6 = x.v6, frag = x.frag;
+    const uint32_t room = x.room, hl = x.hl, proto = x.proto, ip_plen = x.ip_plen;
     const uint32_t ulen = ((g0 & 0xFFu) << 8) | ((g0 >> 8) & 0xFFu);
     const bool ck_zero = (g0 >> 16) == 0u; // udp.c:132
     const uint32_t udp_len = min(ulen, ip_plen); // udp.c:128
     const uint32_t L = udp_len + hl;             // unwrapped; > 65535 is past any frame
-
+    const bool version_ok = x.version_ok, hdr_in = x.hdr_in, udp_in = x.udp_in;
     uint32_t v;
     if (flen < 14u)
         v = kRxTruncated;
@@ -154,6 +140,90 @@ __device__ __forceinline__ RxParse rx_parse(uint64_t fa, uint32_t flen, bool val
     h.verdict = v;
     return h;
 }
+
+// Steps 1 and 2 in ONE load round: the frame's first five aligned chunks
+// (frame bytes [0, 65) at least, each chunk loaded only if it overlaps the
+// frame) hold the Ethernet header, an IPv4 header of up to 40 bytes or the
+// IPv6 header, and the UDP length / checksum fields after either.  A lane
+// with a longer IPv4 header (options > 20 B) or a malformed IHL < 5 sets
+// `slow` and is re-parsed by rx_parse_slow.  Two dependent load rounds per tile cost the mixed-size ring
+// its headroom over payload_cksum alone.
+__device__ __forceinline__ RxParse rx_parse(uint64_t fa, uint32_t flen, bool valid, uint64_t zero,
+                                            bool &slow)
+{
+    const uint64_t fend = fa + flen;
+    const uint64_t cf = fa & ~15ull;
+    const uint32_t sf = (uint32_t)(fa & 15u);
+    u32x4 c[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+        c[k] = load_chunk<false>(valid && cf + 16ull * k < fend ? cf + 16ull * k : zero);
+    // frame bytes 12..23 start in chunk 0 or 1
+    const uint32_t o1 = sf + 12u;
+    const bool j1 = o1 >= 16u;
+    const u32x4 x1 = j1 ? c[1] : c[0], y1 = j1 ? c[2] : c[1];
+    uint32_t fw[3];
+    win_rot(x1, y1, y1, o1 & 15u, fw);
+    const RxHdr x = rx_hdr(fw[0], fw[1], fw[2], flen);
+    slow = valid && x.hdr_in && x.v4 && (x.hl > 40u || x.hl < 20u);
+    // UDP length / checksum at frame byte 14 + hl + 4: chunk 2, 3 or 4 (20 <= hl <= 40)
+    const uint32_t u = sf + 18u + x.hl;
+    const uint32_t ju = min(u >> 4, 4u);
+    const u32x4 z4 = {0u, 0u, 0u, 0u};
+    const u32x4 xu = ju <= 2u ? c[2] : (ju == 3u ? c[3] : c[4]);
+    const u32x4 yu = ju <= 2u ? c[3] : (ju == 3u ? c[4] : z4);
+    const uint32_t g0 = win_bytes(xu, yu, yu, u & 15u, 0);
+    // ip_cksum(ip, hl) (ip4.c:110-115) over frame bytes [14, 14 + hl), as in
+    // rx_parse_slow; 14 + 40 + 15 < 80: inside the five chunks.
+    uint32_t V = 0;
+    if (x.v4 && x.hdr_in) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k)
+            V += seg_range(c[k], 16 * k - (int)(sf + 14u), 0, (int)min(x.hl, 40u));  // (slow lanes: redone)
+    }
+    const uint16_t ipck = fold_not(((fa + 14u) & 1u) ? __builtin_amdgcn_alignbit(V, V, 24) : V);
+    return rx_decide(fa, flen, valid, x, g0, ipck);
+}
+
+// Steps 1 and 2 in two load rounds for this lane's frame [fa, fa + flen): the
+// chunks around frame bytes 12..23 first, then, with the IHL known, the UDP
+// fields and the IPv4 header's chunks (any IHL).  The fallback of rx_parse.
+__device__ __forceinline__ RxParse rx_parse_slow(uint64_t fa, uint32_t flen, bool valid,
+                                                 uint64_t zero)
+{
+    const uint64_t fend = fa + flen;
+    const uint64_t a1 = fa + 12u;
+    const Win2 w1 = win2_load(a1, fend, valid && flen > 12u, zero);
+    const uint32_t s1 = (uint32_t)(a1 & 15u);
+    uint32_t fw[3]; // frame 12..15, 16..19 = ip 2..5, 20..23 = ip 6..9
+    win_rot(w1.x, w1.y, w1.y, s1, fw);
+    const RxHdr x = rx_hdr(fw[0], fw[1], fw[2], flen);
+    const uint64_t ip = fa + 14u;
+    const uint32_t hl = x.hl;
+    // The UDP length / checksum fields (udp.h:41-46) at ip + hl + 4, and the
+    // IPv4 header's chunks, all issued before any is used.
+    const uint64_t a2 = ip + hl + 4u;
+    const Win2 w2 = win2_load(a2, fend, valid && x.udp_in, zero);
+    const bool hsum = valid && x.hdr_in && x.v4;
+    const uint32_t sip = (uint32_t)(ip & 15u);
+    const uint64_t cip = ip & ~15ull;
+    const uint32_t nh = hsum ? (sip + hl + 15u) >> 4 : 0u;
+    u32x4 hc[kHdrChunks];
+#pragma unroll
+    for (int k = 0; k < kHdrChunks; ++k)
+        hc[k] = load_chunk<false>((uint32_t)k < nh ? cip + 16ull * k : zero);
+    // ip_cksum(ip, hl) (ip4.c:110-115): word sum at even addresses; an odd
+    // start folds rotl32(V, 8) (the seg path's residue identity; <= 30 words,
+    // no wrap).
+    uint32_t V = 0;
+#pragma unroll
+    for (int k = 0; k < kHdrChunks; ++k)
+        V += seg_range(hc[k], 16 * k - (int)sip, 0, (int)hl);
+    const uint16_t ipck = fold_not((ip & 1u) ? __builtin_amdgcn_alignbit(V, V, 24) : V);
+    const uint32_t g0 = win_bytes(w2.x, w2.y, w2.y, (uint32_t)(a2 & 15u), 0);
+    return rx_decide(fa, flen, valid, x, g0, ipck);
+}
+
 
 // UNS: 64-chunk rows per row group of the gathered stream (4, as the seg
 // kernel's ragged default).
@@ -191,7 +261,13 @@ k_rx_verdict(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
         const uint32_t flen = flen_n;
         meta_load(offs, flens, (tile + nwaves) * 64 + lane, n, off_n, flen_n);
 
-        const RxParse h = rx_parse(fa, flen, valid, zero);
+        bool slow = false;
+        RxParse h = rx_parse(fa, flen, valid, zero, slow);
+        if (__ballot(slow)) { // IPv4 headers with more than 20 B of options
+            const RxParse hs = rx_parse_slow(fa, flen, slow, zero);
+            if (slow)
+                h = hs;
+        }
         uint32_t v = h.verdict;
         if (__ballot(h.need)) {
             // payload_cksum(ip, udp_len + hl) of the frames that need it, as a
