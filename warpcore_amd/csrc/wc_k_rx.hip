@@ -141,23 +141,28 @@ __device__ __forceinline__ RxParse rx_decide(uint64_t fa, uint32_t flen, bool va
     return h;
 }
 
-// Steps 1 and 2 in ONE load round: the frame's first five aligned chunks
+// Steps 1 and 2 in ONE load round (rx_load, then rx_parse on what it
+// loaded): the frame's first five aligned chunks
 // (frame bytes [0, 65) at least, each chunk loaded only if it overlaps the
 // frame) hold the Ethernet header, an IPv4 header of up to 40 bytes or the
 // IPv6 header, and the UDP length / checksum fields after either.  A lane
 // with a longer IPv4 header (options > 20 B) or a malformed IHL < 5 sets
 // `slow` and is re-parsed by rx_parse_slow.  Two dependent load rounds per tile cost the mixed-size ring
 // its headroom over payload_cksum alone.
-__device__ __forceinline__ RxParse rx_parse(uint64_t fa, uint32_t flen, bool valid, uint64_t zero,
-                                            bool &slow)
+__device__ __forceinline__ void rx_load(uint64_t fa, uint32_t flen, bool valid, uint64_t zero,
+                                        u32x4 (&c)[5])
 {
     const uint64_t fend = fa + flen;
     const uint64_t cf = fa & ~15ull;
-    const uint32_t sf = (uint32_t)(fa & 15u);
-    u32x4 c[5];
 #pragma unroll
     for (int k = 0; k < 5; ++k)
         c[k] = load_chunk<false>(valid && cf + 16ull * k < fend ? cf + 16ull * k : zero);
+}
+
+__device__ __forceinline__ RxParse rx_parse(const u32x4 (&c)[5], uint64_t fa, uint32_t flen,
+                                            bool valid, bool &slow)
+{
+    const uint32_t sf = (uint32_t)(fa & 15u);
     // frame bytes 12..23 start in chunk 0 or 1
     const uint32_t o1 = sf + 12u;
     const bool j1 = o1 >= 16u;
@@ -179,7 +184,7 @@ __device__ __forceinline__ RxParse rx_parse(uint64_t fa, uint32_t flen, bool val
     if (x.v4 && x.hdr_in) {
 #pragma unroll
         for (int k = 0; k < 5; ++k)
-            V += seg_range(c[k], 16 * k - (int)(sf + 14u), 0, (int)min(x.hl, 40u));  // (slow lanes: redone)
+            V += seg_range(c[k], 16 * k - (int)(sf + 14u), 0, (int)min(x.hl, 40u));
     }
     const uint16_t ipck = fold_not(((fa + 14u) & 1u) ? __builtin_amdgcn_alignbit(V, V, 24) : V);
     return rx_decide(fa, flen, valid, x, g0, ipck);
@@ -261,29 +266,52 @@ k_rx_verdict(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
         const uint32_t flen = flen_n;
         meta_load(offs, flens, (tile + nwaves) * 64 + lane, n, off_n, flen_n);
 
+        // Header chunks first; then every frame that may need the UDP check
+        // (>= 28 IP bytes) streams its IP bytes [ip, ip + room) as the seg
+        // path's gathered stream, and the parse completes once that stream's
+        // first row group is in flight (seg_tile's Late hook): the checked
+        // range [ip, ip + udp_len + hl) is a prefix of the streamed one.
+        // Frames that turn out not to need the check were read for nothing.
+        u32x4 c[5];
+        rx_load(fa, flen, valid, zero, c);
+        const uint64_t ip = fa + 14u;
+        const uint32_t room = flen >= 14u ? flen - 14u : 0u;
+        const bool spec = valid && room >= 28u;
         bool slow = false;
-        RxParse h = rx_parse(fa, flen, valid, zero, slow);
-        if (__ballot(slow)) { // IPv4 headers with more than 20 B of options
-            const RxParse hs = rx_parse_slow(fa, flen, slow, zero);
-            if (slow)
-                h = hs;
-        }
-        uint32_t v = h.verdict;
-        if (__ballot(h.need)) {
-            // payload_cksum(ip, udp_len + hl) of the frames that need it, as a
-            // gathered stream (every other lane is an empty packet in it).
-            const uint32_t span = h.need ? max(h.plen, 20u) : 0u;
-            const FlatTile t = flat_tile_setup<UNS, 1>(L.f, lane, h.ip, h.plen, span, h.need, 0u);
+        RxParse h{};
+        uint32_t v;
+        if (__ballot(spec)) {
+            const FlatTile t = flat_tile_setup<UNS, 1>(L.f, lane, ip, room, room, spec, 0u);
+            bool need = false;
+            auto late = [&](uint32_t &len, bool &on) {
+                h = rx_parse(c, fa, flen, valid, slow);
+                need = h.need && !slow;
+                on = need;
+                len = need ? h.plen : 0u;
+            };
             bool done = true;
             uint16_t rh = 0;
-            uint16_t r = seg_tile<UNS, WC_KIND_PAYLOAD, NT, false, GathSrc<UNS, NT>, true>(
-                L.f.pre, L.stage, L.pm, lane, h.ip, 16ull * t.cp + (h.ip & 15u), h.plen, h.need,
-                t.total, GathSrc<UNS, NT>{&L.f, t}, zero, done, rh);
-            if (h.need && !done) // header longer than the packet, or a possible wrap
-                r = lane_payload_exact<NT>(h.ip, h.plen);
-            if (h.need)
+            uint16_t r = seg_tile<UNS, WC_KIND_PAYLOAD, NT, false, GathSrc<UNS, NT>, true,
+                                  decltype(late)>(
+                L.f.pre, L.stage, L.pm, lane, ip, 16ull * t.cp + (ip & 15u), room, spec,
+                t.total, GathSrc<UNS, NT>{&L.f, t}, zero, done, rh, late);
+            if (need && !done) // header longer than the packet, or a possible wrap
+                r = lane_payload_exact<NT>(ip, h.plen);
+            v = h.verdict;
+            if (need)
                 v = r != 0 ? kRxBadUdpCksum : kRxOk; // udp.c:134-139
             wave_order(); // the tables are rewritten by the next tile
+        } else {
+            h = rx_parse(c, fa, flen, valid, slow);
+            v = h.verdict;
+        }
+        if (__ballot(slow)) { // IPv4 headers with more than 20 B of options, IHL < 5
+            const RxParse hs = rx_parse_slow(fa, flen, slow, zero);
+            if (slow) {
+                v = hs.verdict;
+                if (hs.need)
+                    v = lane_payload_exact<NT>(hs.ip, hs.plen) != 0 ? kRxBadUdpCksum : kRxOk;
+            }
         }
         if (valid)
             verdict[p] = (uint8_t)v;

@@ -301,24 +301,35 @@ struct GathSrc {
 // seg arithmetic can't take gets done = false on its own, the others keep
 // their result, and the caller recomputes that lane's packet exactly
 // (lane_payload_exact) -- no flat path in that kernel.
-template <int UNS, int KIND, bool NT, bool HDR, class Src, bool LANEFIX = false>
+struct NoLate {
+    __device__ __forceinline__ void operator()(uint32_t &, bool &) const {}
+};
+
+template <int UNS, int KIND, bool NT, bool HDR, class Src, bool LANEFIX = false,
+          class Late = NoLate>
 __device__ __forceinline__ uint16_t seg_tile(uint32_t *pre, u32x4 *stage, const u32x4 *pm,
                                              int lane, uint64_t a, uint64_t ra, uint32_t len,
                                              bool valid, uint32_t T, const Src &src,
-                                             uint64_t zero, bool &done, uint16_t &rh)
+                                             uint64_t zero, bool &done, uint16_t &rh,
+                                             const Late &late = Late{})
 {
     constexpr uint32_t kGrp = 64u * UNS;
     constexpr bool PL = KIND == WC_KIND_PAYLOAD;
     constexpr int HC = PL ? (HDR ? 3 : 2) : 0;
     constexpr bool CL = Src::kClamp;
-    const uint64_t rs = ra + (PL ? 8u : 0u), re = ra + len;
-    const uint32_t cs = (uint32_t)(rs >> 4), qs = (uint32_t)(rs & 15u);
-    const uint32_t ce = (uint32_t)(re >> 4), qe = (uint32_t)(re & 15u);
     const uint32_t c0 = (uint32_t)(ra >> 4);
     const uint32_t sa = (uint32_t)(ra & 15u); // == a & 15 (dense and gathered streams)
 
     SegRows<UNS> A, B;
     src.issue(A, 0, lane);
+    // Late: the lane's packet length (and whether it is summed at all) may be
+    // decided only now, with the first row group in flight -- the stream
+    // already holds the longest range the packet can have (the RX verdict
+    // kernel streams each frame while its headers are still being parsed).
+    late(len, valid);
+    const uint64_t rs = ra + (PL ? 8u : 0u), re = ra + len;
+    const uint32_t cs = (uint32_t)(rs >> 4), qs = (uint32_t)(rs & 15u);
+    const uint32_t ce = (uint32_t)(re >> 4), qe = (uint32_t)(re & 15u);
 
     uint32_t carry = 0, Ps = 0, Pe = 0;
     u32x4 hs = {0u, 0u, 0u, 0u}, he = {0u, 0u, 0u, 0u}, h1 = {0u, 0u, 0u, 0u},
