@@ -28,6 +28,7 @@ for c in ${CASES:-c2:ip c2:payload}; do
         rslot) a="--config c3 --len 1500 --stride 2048 --offset 14 --ragged" ;;
         rc2) a="--config c2 --ragged" ;;
         c3-*) a="--config c3 --len ${cfg#c3-}" ;;
+        s14-*) a="--config c3 --len ${cfg#s14-} --stride 2048 --offset 14" ;;
     esac
     echo "== $c"
     log=gpurun_out/ab_${cfg}_${kind}${hdr:+_h}.log

@@ -275,17 +275,28 @@ int ensure_device(Device **out, Config *cfg)
 // ---------------------------------------------------------------------------
 // Planner.
 
-wc::Shape shape_for_chunks(uint32_t nch, bool full, bool payload, bool aligned)
+wc::Shape shape_for_chunks(uint32_t nch, bool full, bool payload, bool aligned,
+                           bool sparse = false)
 {
     // Smallest group covering the packet in one pass, with U packets per
     // group so every lane keeps ~4-18 16-byte loads in flight (tuned on
     // MI355X: DESIGN.md section 5, profiles/tune_r01_*.log).
     if (nch <= 4)
         return {4, 1, 4};
+    // Sparse batches (stride >= twice the packet's chunk span: netmap slots)
+    // run at the rate of the cache lines they touch, one or two per packet;
+    // shapes with more lanes per packet reach it (2048-B slots at +14,
+    // profiles/ab_r03_slot_shapes.log): ip_cksum 5-6 chunks on 8 x 1 x 4
+    // (64 / 72 / 80 B: 36 -> 41, 41 -> 47, 46 -> 52 %), payload_cksum 9-16
+    // chunks on 8 x 2 x 4 (128 / 160 / 200 / 240 B: 37 -> 40, 46 -> 51,
+    // 57 -> 62, 69 -> 76 %).  payload_cksum keeps 4 x 2 x 2 at 5-6 chunks
+    // (8 x 1 x 4: 36 -> 28 %).
     if (nch <= 6)
-        return {4, 2, 2};
+        return sparse && !payload ? wc::Shape{8, 1, 4} : wc::Shape{4, 2, 2};
     if (nch <= 8)
         return {8, 1, 4};
+    if (sparse && payload && nch <= 16)
+        return {8, 2, 4};
     // 9..24 chunks: 8 lanes x 3 chunks, two packets per group -- fewer dead
     // lane slots than 16 x 2 (tools/sweep_mid.sh: 256 B 78.7 -> 84.1 %,
     // 200 B 55 -> 67.5 %, 256 B at +14 50 -> 60 % of HBM peak)
@@ -404,7 +415,8 @@ Plan plan_strided(const Device &D, const Config &C, uint64_t base, uint64_t stri
     p.full = kind == WC_CKSUM_IP && base % 16 == 0 && stride % 16 == 0 &&
              len % 16 == 0 && !(C.variant & 2);
     p.shape = C.have_shape ? C.shape
-                           : shape_for_chunks(nch, p.full, kind == WC_CKSUM_PAYLOAD, phase == 0);
+                           : shape_for_chunks(nch, p.full, kind == WC_CKSUM_PAYLOAD, phase == 0,
+                                              stride >= 32ull * nch);
     p.grid = grid_for(D, C, p.shape, n);
     // Packed (or nearly packed) packets that the group kernel would have to
     // mask: the seg kernel streams their byte range instead (k_cksum_seg<STR>)
