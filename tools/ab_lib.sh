@@ -21,6 +21,7 @@ for c in ${CASES:-c4:payload}; do
         rslot) a="--config c3 --len 1500 --stride 2048 --offset 14 --ragged" ;;
         rc2) a="--config c2 --ragged" ;;
         c3-*) a="--config c3 --len ${cfg#c3-}" ;;
+        s14-*) a="--config c3 --len ${cfg#s14-} --stride 2048 --offset 14" ;;
     esac
     echo "== $c"
     for rep in 1 2; do

@@ -2,6 +2,8 @@
 // k_cksum and its launch table.
 #include "wc_device.h"
 
+#include <type_traits>
+
 namespace wc {
 
 // ---------------------------------------------------------------------------
@@ -39,6 +41,20 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
     constexpr int GPW = 64 / G;
     constexpr uint64_t PPW = (uint64_t)GPW * U;
     constexpr int PASS = G * CPL;
+    // payload_cksum as ip_cksum over [8, len) plus per-packet terms from the
+    // header (payload_as_ip, wc_flat.h; the lean kernel's scheme): the
+    // chunk sums no longer wait for the header hand-off, and their masks are
+    // ip_cksum's.  A round with a packet the terms do not cover (IPv4 with
+    // options or IHL < 5, a packet shorter than its header) is summed again
+    // from the same registers with the header ranges (wave-uniform, rare in
+    // real traffic).  The fused header variant keeps the header-range
+    // accumulate (it sums [0, hl) too), and so do all shapes but the 96-chunk
+    // passes (32 x 3, 16 x 6: MTU packets), where it measured faster -- 1500 B
+    // in 2048-B slots at +14 85.9 -> 89.7 %, C2 92.3 -> 92.7 % -- and not
+    // slower elsewhere (2048-B slots at +14: 128 B 41.4 -> 37.3 %, 576 B 78 ->
+    // 75.6 %, 1024 B on 16 x 5 77.3 -> 69.1 %, 9000 B on 32 x 18 92 -> 26 %:
+    // profiles/ab_r03_strided_asip.log).
+    constexpr bool ASIP = KIND == WC_KIND_PAYLOAD && !HDR && G * CPL == 96;
 
     const int lane = threadIdx.x & 63;
     const int gl = lane & (G - 1);
@@ -111,82 +127,104 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             PseudoHdr ph{0u, 1u, 0u};
+            uint32_t extra = 0;
+            bool ok = true;
             if constexpr (KIND == WC_KIND_PAYLOAD) {
-                // Header bytes 0, 2, 3, 6 sit in the group's chunks 0/1, i.e.
-                // in d[u][0] of group lanes 0 and 1.
+                // Header bytes 0..11 sit in the group's chunks 0/1, i.e. in
+                // d[u][0] of group lanes 0 and 1.
                 const int su = s[u];
-                uint32_t b0, b2, b3, b6;
+                uint32_t b0, b2, b3, b6, x1 = 0, x2 = 0;
                 auto exchange = [&] { // ds_bpermute from the lane holding each byte
                     b0 = __shfl(pick_byte(d[u][0], su), lead + (su >> 4), 64);
                     b2 = __shfl(pick_byte(d[u][0], (su + 2) & 15), lead + ((su + 2) >> 4), 64);
                     b3 = __shfl(pick_byte(d[u][0], (su + 3) & 15), lead + ((su + 3) >> 4), 64);
                     b6 = __shfl(pick_byte(d[u][0], (su + 6) & 15), lead + ((su + 6) >> 4), 64);
                 };
-                {
-                    if (!(variant & (1 << 19))) {
-                        // DPP broadcasts of the three window dwords that
-                        // hold packet bytes 0..7 (window dword k is dword
-                        // k & 3 of group lane k >> 2); the ds_bpermute
-                        // exchange (WC_VARIANT bit 19) cost 2048-B netmap
-                        // slots 4 points, packed 64-192 B 2-5 points
-                        // (profiles/ab_r02_hdr_dpp.log).
-                        uint32_t w[3];
+                if (ASIP || !(variant & (1 << 19))) {
+                    // DPP broadcasts of the window dwords that hold packet
+                    // bytes 0..7 (0..11 for ASIP) (window dword k is dword
+                    // k & 3 of group lane k >> 2); the ds_bpermute exchange
+                    // (WC_VARIANT bit 19) cost 2048-B netmap slots 4 points,
+                    // packed 64-192 B 2-5 points (profiles/ab_r02_hdr_dpp.log).
+                    constexpr int NW = ASIP ? 4 : 3;
+                    uint32_t w[NW];
 #pragma unroll
-                        for (int j = 0; j < 3; ++j) {
-                            const int k = (su >> 2) + j;
-                            const uint32_t mine = pick_dword(d[u][0], k & 3);
-                            // both broadcasts run with every lane active
-                            const uint32_t f0 = group_bcast<G, 0>(mine);
-                            const uint32_t f1 = group_bcast<G, 1>(mine);
-                            w[j] = (k >> 2) ? f1 : f0;
-                        }
-                        const uint32_t sh = 8u * (uint32_t)(su & 3);
-                        const uint32_t x0 = __builtin_amdgcn_alignbit(w[1], w[0], sh); // 0..3
-                        const uint32_t x1 = __builtin_amdgcn_alignbit(w[2], w[1], sh); // 4..7
-                        b0 = x0 & 0xFFu;
-                        b2 = (x0 >> 16) & 0xFFu;
-                        b3 = x0 >> 24;
-                        b6 = (x1 >> 16) & 0xFFu;
-                    } else {
-                        exchange();
+                    for (int j = 0; j < NW; ++j) {
+                        const int k = (su >> 2) + j;
+                        const uint32_t mine = pick_dword(d[u][0], k & 3);
+                        // both broadcasts run with every lane active
+                        const uint32_t f0 = group_bcast<G, 0>(mine);
+                        const uint32_t f1 = group_bcast<G, 1>(mine);
+                        w[j] = (k >> 2) ? f1 : f0;
                     }
+                    const uint32_t sh = 8u * (uint32_t)(su & 3);
+                    const uint32_t x0 = __builtin_amdgcn_alignbit(w[1], w[0], sh); // 0..3
+                    x1 = __builtin_amdgcn_alignbit(w[2], w[1], sh);                // 4..7
+                    if constexpr (ASIP)
+                        x2 = __builtin_amdgcn_alignbit(w[3], w[2], sh); // 8..11
+                    b0 = x0 & 0xFFu;
+                    b2 = (x0 >> 16) & 0xFFu;
+                    b3 = x0 >> 24;
+                    b6 = (x1 >> 16) & 0xFFu;
+                } else {
+                    exchange();
                 }
                 ph = pseudo_hdr(b0, b2, b3, b6);
-            }
-            const int rs = (int)ph.hl, re = (int)plen[u];
-
-            uint32_t E = 0, O = 0, Eh = 0, Oh = 0;
-#pragma unroll
-            for (int c = 0; c < CPL; ++c)
-                accum_strided<KIND, FULL, HDR>(d[u][c], 16 * (gl + c * G) - s[u], rs, re,
-                                               (uint32_t)(gl + c * G) < nch[u], ph.v4, E, O,
-                                               Eh, Oh);
-            // Packets longer than one pass (e.g. 9000 B jumbo frames).
-            for (uint32_t kb = PASS; kb < nch[u]; kb += PASS) {
-                u32x4 t[CPL];
-#pragma unroll
-                for (int c = 0; c < CPL; ++c) {
-                    const uint32_t k = kb + (uint32_t)(gl + c * G);
-                    t[c] = load_chunk<NT>(k < nch[u] ? c0[u] + 16ull * k : zero);
+                if constexpr (ASIP) {
+                    ok = ph.v4 ? ph.hl == 20u && plen[u] >= 20u : plen[u] >= 40u;
+                    extra = ph.v4 ? ph.special - ((x2 & 0xFFu) + ((x2 >> 16) & 0xFFu) +
+                                                  ((x2 >> 24) << 8))
+                                  : ph.special + (x1 & 0xFFFFu);
                 }
+            }
+            const int re = (int)plen[u];
+            uint32_t E = 0, O = 0, Eh = 0, Oh = 0;
+            // The chunk sums of [rs, re) with kind K's weights, extra passes
+            // for packets longer than one (e.g. 9000 B jumbo frames) reloaded.
+            auto sum_packet = [&](auto kind, int rs) {
+                constexpr int K = decltype(kind)::value;
 #pragma unroll
                 for (int c = 0; c < CPL; ++c)
-                    accum_strided<KIND, FULL, HDR>(t[c], 16 * (int)(kb + gl + c * G) - s[u],
-                                                   rs, re, kb + (uint32_t)(gl + c * G) < nch[u],
-                                                   ph.v4, E, O, Eh, Oh);
+                    accum_strided<K, FULL, HDR>(d[u][c], 16 * (gl + c * G) - s[u], rs, re,
+                                                (uint32_t)(gl + c * G) < nch[u], ph.v4, E, O,
+                                                Eh, Oh);
+                for (uint32_t kb = PASS; kb < nch[u]; kb += PASS) {
+                    u32x4 t[CPL];
+#pragma unroll
+                    for (int c = 0; c < CPL; ++c) {
+                        const uint32_t k = kb + (uint32_t)(gl + c * G);
+                        t[c] = load_chunk<NT>(k < nch[u] ? c0[u] + 16ull * k : zero);
+                    }
+#pragma unroll
+                    for (int c = 0; c < CPL; ++c)
+                        accum_strided<K, FULL, HDR>(t[c], 16 * (int)(kb + gl + c * G) - s[u],
+                                                    rs, re, kb + (uint32_t)(gl + c * G) < nch[u],
+                                                    ph.v4, E, O, Eh, Oh);
+                }
+            };
+            uint32_t S;
+            if constexpr (ASIP) {
+                sum_packet(std::integral_constant<int, WC_KIND_IP>{}, 8);
+                S = combine(E, O, s[u] & 1) + (gl == 0 ? extra : 0u);
+                if (__ballot(valid[u] && !ok)) { // rare: redo the round with header ranges
+                    E = O = 0;
+                    sum_packet(std::integral_constant<int, WC_KIND_PAYLOAD>{}, (int)ph.hl);
+                    S = combine(E, O, s[u] & 1) + (gl == 0 ? ph.special : 0u);
+                }
+            } else {
+                sum_packet(std::integral_constant<int, KIND>{}, KIND == WC_KIND_PAYLOAD ? (int)ph.hl : 0);
+                S = combine(E, O, s[u] & 1) + (gl == 0 ? ph.special : 0u);
             }
-
-            uint32_t S = combine(E, O, s[u] & 1);
-            S += gl == 0 ? ph.special : 0u;
             S = group_sum<G>(S);
             uint32_t Sh = 0;
             if constexpr (HDR)
                 Sh = group_sum<G>(combine(Eh, Oh, s[u] & 1));
+            const uint32_t rr = fold_not(S);
             if (lane_store) {
                 // Lane j of the wave takes packet p0 + j's result from its
                 // group (every lane of a group holds the sum).
                 const int src = (lane % GPW) * G;
-                const uint32_t r = __shfl((uint32_t)fold_not(S), src, 64);
+                const uint32_t r = __shfl(rr, src, 64);
                 if (lane / GPW == u)
                     res = r;
                 if constexpr (HDR) {
@@ -198,7 +236,7 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
             }
             if (gl == 0 && valid[u]) {
                 const uint64_t i = p0 + (uint64_t)u * GPW + grp;
-                const uint16_t r = fold_not(S);
+                const uint16_t r = (uint16_t)rr;
                 if (out && !(variant & 64)) // WC_VARIANT bit 64: no result store (timing only)
                     out[i] = r;
                 nbad += r != 0;
@@ -209,9 +247,10 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
         if (lane_store) {
             const uint64_t i = p0 + (uint64_t)lane;
             if (lane < (int)PPW && i < n) {
+                const uint16_t r = (uint16_t)res;
                 if (out && !(variant & 64)) // WC_VARIANT bit 64: no result store (timing only)
-                    out[i] = (uint16_t)res; // (a nontemporal store measured the same)
-                nbad += res != 0;
+                    out[i] = r; // (a nontemporal store measured the same)
+                nbad += r != 0;
                 if constexpr (HDR)
                     out_hdr[i] = (uint16_t)res_h; // ip4.c:110-115
             }
