@@ -16,9 +16,11 @@ stop_if_fault() {  # $1 = exit code, $2 = step
 }
 
 echo "== smoke" | tee "$OUT/summary.log"
-timeout -k 10 420 python -c "import __graft_entry__ as g; g.build(); g.smoke()" \
+timeout -k 10 420 python -c "import __graft_entry__ as g; g.build(); g.smoke(); \
+print('loaded:', sorted({l.split()[-1] for l in open('/proc/self/maps') if 'wccksum' in l}))" \
     > "$OUT/smoke.log" 2>&1
-rc=$?; tail -3 "$OUT/smoke.log" | tee -a "$OUT/summary.log"; stop_if_fault $rc smoke
+rc=$?; tail -4 "$OUT/smoke.log" | tee -a "$OUT/summary.log"; stop_if_fault $rc smoke
+git_sha=$(cat .head_sha 2>/dev/null || echo unknown); echo "tree: $git_sha" | tee -a "$OUT/summary.log"
 
 echo "== pytest -m gpu" | tee -a "$OUT/summary.log"
 timeout -k 10 900 python -m pytest tests -m gpu -q ${PYTEST_ARGS:-} \
