@@ -716,7 +716,7 @@ int run_ragged_any(const Device &D, const Config &C, const uint8_t *d_base, cons
 {
     if (kind == kKindRx)
         return hip_err(wc::launch_rx_verdict(d_base, d_off, d_len, n, (uint8_t *)d_out, nullptr,
-                                             C.nt != 0, st));
+                                             C.nt != 0, st, C.variant));
     const Plan p = plan_ragged(D, C, n, kind, zero_copy);
     wc::LaunchArgs a{d_base, 0,       0,    d_off, d_len, n,
                      (uint16_t *)d_out, nullptr, kind, true,  false, C.nt != 0,
@@ -1253,7 +1253,7 @@ int wc_rx_verdict_ragged(const void *d_base, const uint64_t *d_off, const uint16
     if (rc)
         return rc;
     return hip_err(wc::launch_rx_verdict(d_base, d_off, d_frame_len, n, d_verdict, d_drops,
-                                         C.nt != 0, (hipStream_t)stream));
+                                         C.nt != 0, (hipStream_t)stream, C.variant));
 }
 
 int wc_rx_verdict_host(const void *h_base, uint64_t h_bytes, const uint64_t *h_off,

@@ -167,6 +167,6 @@ hipError_t launch_synth(void *buf, uint64_t nbytes, uint64_t seed, int grid,
 // drops (optional) accumulates the frames the reference's RX path drops.
 hipError_t launch_rx_verdict(const void *base, const uint64_t *offs, const uint16_t *flens,
                              uint64_t n, uint8_t *verdict, uint64_t *drops, bool nt,
-                             hipStream_t st);
+                             hipStream_t st, int variant = 0);
 
 } // namespace wc

@@ -328,8 +328,9 @@ k_rx_verdict(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
 
 hipError_t launch_rx_verdict(const void *base, const uint64_t *offs, const uint16_t *flens,
                              uint64_t n, uint8_t *verdict, uint64_t *drops, bool nt,
-                             hipStream_t st)
+                             hipStream_t st, int variant)
 {
+    (void)variant; // (tuning build: A/B branches)
     const uint64_t tiles = (n + 63) / 64;
     const int grid = (int)std::min<uint64_t>(
         kMaxGridBlocks, std::max<uint64_t>(1, (tiles + kFlatWaves - 1) / kFlatWaves));
