@@ -480,6 +480,40 @@ def test_strided_packed_seg_wild_payload(gpu, monkeypatch, length):
             np.testing.assert_array_equal(got, want, err_msg=f"stride {stride} start {start}")
 
 
+@pytest.mark.parametrize("length,stride,start", [(1472, 1472, 0), (1500, 2048, 14),
+                                                  (1472, 2048, 1), (1536, 2048, 0)])
+def test_payload_strided_mtu_header_terms(gpu, length, stride, start):
+    """payload_cksum on the 96-chunk group shapes (32 x 3, 16 x 6), which sum
+    [8, len) with ip_cksum's masks and add the header terms at the end: a
+    round holding an IPv4 header with options, a malformed IHL or a short
+    packet is summed again with header ranges.  Every header kind in every
+    round position, IPv6 next_hdr 254 / 255 (the uint32 wrap), both parities
+    of the start, against the oracle."""
+    rng = np.random.default_rng(length + stride + start)
+    n = 1500
+    buf = rng.integers(0, 256, n * stride + 64, dtype=np.uint8)
+    for i in range(n):
+        o = start + i * stride
+        k = (i * 7) % 11
+        if k < 5:
+            pkt, ln = (ipv6_udp if k % 2 else ipv4_udp)(
+                rng.integers(0, 256, length - 28 - (20 if k % 2 else 0),
+                             dtype=np.uint8).tobytes(), rng)
+            buf[o:o + ln] = np.frombuffer(pkt, np.uint8)
+        elif k == 5:
+            buf[o] = 0x40 | int(rng.integers(6, 16))   # IPv4 with options
+        elif k == 6:
+            buf[o] = 0x40 | int(rng.integers(0, 5))    # malformed IHL < 5
+        elif k == 7:
+            buf[o] = 0x60                              # IPv6, next_hdr 254 / 255
+            buf[o + 6] = 254 + (i & 1)
+        # k 8..10: random bytes as they are
+    d = dev_u8(buf, gpu)
+    got = host(wc.cksum_strided(d, stride, length, n, kind="payload", byte_offset=start))
+    want = c_oracle.cksum_strided(buf, stride, length, n, kind=1, byte_offset=start)
+    np.testing.assert_array_equal(got, want)
+
+
 @pytest.mark.parametrize("length,stride", [(700, 2048), (1000, 1003), (1500, 1500),
                                            (1500, 2048), (3000, 3001), (3000, 4096),
                                            (5000, 5007)])
