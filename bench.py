@@ -12,14 +12,28 @@ meet only at the barriers around the timed region and in the max-over-ranks
 time reduction.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
-                    [--config c2|c3|c4|c5|slots|zslots|rx] [--len L] [--kind ip|payload]
-                    [--headers] [--fused] [--cpu-seconds S] [--no-cpu-baseline] [--no-c5]
+                    [--config c2|c3|c4|c5|slots|zslots|rx|zrx] [--len L] [--kind ip|payload]
+                    [--headers] [--fused] [--batches K] [--rotate-bytes B]
+                    [--cpu-seconds S] [--no-cpu-baseline] [--no-c5] [--no-extra]
 
-Every line also carries a "c5" object: SURVEY C5, the north star's
-strong-scaling curve -- 2^28 x 1472 B in total, split evenly over the N ranks,
-each rank's share checksummed as launches over a resident 2^25-packet (49 GB)
-window -- timed with its own barriers and max over ranks, with sampled
-parity on every rank.  --config c5 makes it the headline instead.
+HBM, not the Infinity Cache: a strided batch smaller than --rotate-bytes
+(1 GiB, 4x the 256 MiB Infinity Cache, MI355X_MICROARCH.md "Infinity Cache")
+is run as K = ceil(1 GiB / batch) distinct batches, each with its own seed,
+step i checksumming batch i mod K, so no step re-reads bytes the cache still
+holds; every packet of every batch is checked.  C2's 1.54 GB batch is K = 1.
+
+Every default line also carries (after the headline's timed region):
+* "c5": SURVEY C5, the north star's strong-scaling curve -- 2^28 x 1472 B in
+  total, split evenly over the N ranks, each rank's share checksummed as
+  launches over a resident 2^25-packet (49 GB) window -- timed with its own
+  barriers and max over ranks, with sampled parity on every rank.
+* "c3": BASELINE configs[2], the MTU sweep 64/256/576/1472/9000 B x 2^20 on
+  rotating batches (>= 1 GiB footprint), each size's frac from HBM plus the
+  single-buffer figure as frac_l3_resident, every packet checked;
+* "c4": BASELINE configs[3], 2^24 Zipf(1) 64-1472 B packets packed, every
+  packet checked;
+* roofline.frac_rotating: C2 over 4 rotating 1.54 GB batches.
+--no-extra skips c3 / c4 / frac_rotating, --no-c5 the C5 leg.
 --fused runs the fused IPv4 header + payload_cksum pass (wc_cksum_ip_udp_*).
 --config rx is the RX verdict pass (wc_rx_verdict_ragged) over a netmap RX
 ring of well-formed UDP frames (2048-B slots, valid IPv4 / IPv6 checksums).
@@ -33,11 +47,13 @@ Rank 0 prints ONE JSON line (see DESIGN.md section 6 for every field).
 from __future__ import annotations
 
 import argparse
+import copy
 import json
 import os
 import sys
 import time
 from pathlib import Path
+from types import SimpleNamespace
 
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
@@ -48,9 +64,11 @@ import torch  # noqa: E402
 METRIC = "GiB/s payload checksummed (device-resident), 1472 B pkts; % of HBM-read peak"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
 GIB = float(1 << 30)
+C3_SIZES = (64, 256, 576, 1472, 9000)  # BASELINE configs[2]
+BATCH_SEED_STEP = 0x9E3779B9  # seed of batch k = rank seed + k * this
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -65,6 +83,8 @@ def parse():
                          "implies --kind payload --headers)")
     ap.add_argument("--no-c5", action="store_true",
                     help="skip the C5 strong-scaling leg every line carries by default")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the c3 / c4 objects and C2's frac_rotating")
     ap.add_argument("--c5-steps", type=int, default=3, help="timed steps of the C5 leg")
     ap.add_argument("--headers", action="store_true",
                     help="stamp well-formed IPv4 / IPv6 UDP headers on every packet "
@@ -72,6 +92,19 @@ def parse():
     ap.add_argument("--total-packets", type=int, default=1 << 28, help="c5 total")
     ap.add_argument("--window-packets", type=int, default=1 << 25, help="c5 resident window")
     ap.add_argument("--packets", type=int, default=1 << 20)
+    ap.add_argument("--batches", type=int, default=0,
+                    help="c2/c3: distinct batches the steps rotate over (0: enough for "
+                         "--rotate-bytes)")
+    ap.add_argument("--rotate-bytes", type=int, default=1 << 30,
+                    help="c2/c3: smallest footprint of the rotating batches (default 1 GiB, "
+                         "4x the Infinity Cache)")
+    ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
+                    help="replay the timed launches from a captured hipGraph (auto: for c3, "
+                         "where a Python launch can take longer than the kernel)")
+    ap.add_argument("--c3-packets", type=int, default=1 << 20, help="packets per c3 size")
+    ap.add_argument("--c4-packets", type=int, default=1 << 24, help="packets of the c4 object")
+    ap.add_argument("--extra-seconds", type=float, default=0.25,
+                    help="timed seconds per c3 / c4 / frac_rotating measurement")
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="total CPU-baseline time budget (all-thread + 1-core trials)")
     ap.add_argument("--cpu-threads", type=int, default=0,
@@ -81,7 +114,7 @@ def parse():
                          "GPU clock has ramped from idle before the timed steps")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--traffic-file", default=str(ROOT / "profiles" / "traffic.json"))
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 def resolve_launch(args, env=None):
@@ -150,10 +183,19 @@ def dist_setup(args):
     return rank, dev_index, world, coll_dev
 
 
+def rotation(batch_bytes: int, args) -> int:
+    """Distinct batches a strided workload rotates over: --batches, else
+    enough that their footprint reaches --rotate-bytes."""
+    if args.batches > 0:
+        return args.batches
+    return max(1, -(-int(args.rotate_bytes) // max(int(batch_bytes), 1)))
+
+
 def make_workload(args, dev, rank, world):
-    """The headline workload of this run on this rank: (step, packets,
-    algorithmic bytes per step, buffer, results, kernel plan, description,
-    config metadata, layout, scaling)."""
+    """The workload of this run on this rank: a namespace with `step(i)` (one
+    launch over batch i mod K), the packets and algorithmic bytes per step,
+    `batches` (K dicts of buf / out / out_hdr), the kernel plan, description,
+    config metadata, layout (`shape`) and scaling."""
     import warpcore_amd as wc
     from warpcore_amd import dist as wdist
     from warpcore_amd import synth
@@ -172,7 +214,7 @@ def make_workload(args, dev, rank, world):
         out = torch.empty(win, dtype=torch.uint16, device=dev)
         counts = [min(win, share - k * win) for k in range(launches)]
 
-        def step():
+        def step(i=0):
             for c in counts:
                 wc.cksum_strided(buf, L, L, c, out=out, kind=kind)
 
@@ -182,7 +224,9 @@ def make_workload(args, dev, rank, world):
         meta = {"packets_total": args.total_packets, "packets_per_gpu": share,
                 "packet_bytes": L, "layout": "strided", "launches_per_step": launches,
                 "kind": kind}
-        return step, share, share * L, buf, out, plan, desc, meta, (L, L), "strong"
+        return SimpleNamespace(step=step, n=share, nbytes=share * L,
+                               batches=[{"buf": buf, "out": out}], plan=plan, desc=desc,
+                               meta=meta, shape=(L, L), scaling="strong")
     if args.config in ("rx", "zrx"):
         # netmap RX ring (backend_netmap.c:379-391): one well-formed UDP
         # frame per 2048-B slot, valid IPv4 header and UDP checksums; one
@@ -203,7 +247,7 @@ def make_workload(args, dev, rank, world):
         drops = torch.zeros(1, dtype=torch.int64, device=dev)
         wc.rx_verdict_ragged(buf, d_off, d_len, out=out, drops=drops)  # validates the layout
 
-        def step():
+        def step(i=0):
             wc.rx_verdict_ragged(buf, d_off, d_len, out=out, check=False, drops=drops)
 
         nbytes = int(f_len.astype(np.uint64).sum())
@@ -216,33 +260,44 @@ def make_workload(args, dev, rank, world):
             meta["packet_bytes"] = args.len + 42  # frame: Ethernet 14 + IP/UDP 28 + payload
         plan = {"kernel": "k_rx_verdict (header parse + gathered seg stream)",
                 "grid": int((n + 255) // 256)}
-        return step, n, nbytes, buf, out, plan, desc, meta, (f_off, f_len), "weak"
+        return SimpleNamespace(step=step, n=n, nbytes=nbytes,
+                               batches=[{"buf": buf, "out": out}], plan=plan, desc=desc,
+                               meta=meta, shape=(f_off, f_len), scaling="weak")
     if args.config in ("c2", "c3"):
         L = 1472 if args.config == "c2" else args.len
         n = args.packets
         nbytes = n * L
-        buf = torch.empty(nbytes + 64, dtype=torch.uint8, device=dev)
-        wc.synth_fill(buf, seed, nbytes=nbytes)
-        if args.headers:
-            synth.stamp_udp_headers(buf, torch.arange(n, device=dev) * L,
-                                    torch.full((n,), L, device=dev))
-        out = torch.empty(n, dtype=torch.uint16, device=dev)
-        out_hdr = torch.empty(n, dtype=torch.uint16, device=dev) if fused else None
+        K = rotation(nbytes, args)
+        batches = []
+        for k in range(K):
+            buf = torch.empty(nbytes + 64, dtype=torch.uint8, device=dev)
+            wc.synth_fill(buf, seed + k * BATCH_SEED_STEP, nbytes=nbytes)
+            if args.headers:
+                synth.stamp_udp_headers(buf, torch.arange(n, device=dev) * L,
+                                        torch.full((n,), L, device=dev))
+            batches.append({"buf": buf, "out": torch.empty(n, dtype=torch.uint16, device=dev),
+                            "out_hdr": torch.empty(n, dtype=torch.uint16, device=dev)
+                            if fused else None})
 
-        def step():
+        def step(i=0):
+            b = batches[i % K]
             if fused:
-                wc.cksum_ip_udp_strided(buf, L, L, n, out_hdr=out_hdr, out=out)
+                wc.cksum_ip_udp_strided(b["buf"], L, L, n, out_hdr=b["out_hdr"], out=b["out"])
             else:
-                wc.cksum_strided(buf, L, L, n, out=out, kind=kind)
+                wc.cksum_strided(b["buf"], L, L, n, out=b["out"], kind=kind)
 
-        plan = wc.plan_strided(buf.data_ptr(), L, L, n, kind=kind)
+        plan = wc.plan_strided(batches[0]["buf"].data_ptr(), L, L, n, kind=kind)
         desc = (f"C2: {n} x {L} B packets, stride {L}, device-resident"
                 if args.config == "c2" else f"C3: {n} x {L} B packets, stride {L}")
-        meta = {"packets_per_gpu": n, "packet_bytes": L, "layout": "strided", "kind": kind}
+        if K > 1:
+            desc += (f"; steps rotate over {K} distinct batches ({K * nbytes / GIB:.2f} GiB, "
+                     f"past the 256 MiB Infinity Cache)")
+        meta = {"packets_per_gpu": n, "packet_bytes": L, "layout": "strided", "kind": kind,
+                "batches": K, "footprint_bytes": K * nbytes}
         if fused:
             desc += ", fused IPv4 header + payload_cksum pass"
-            meta["out_hdr"] = out_hdr
-        return step, n, nbytes, buf, out, plan, desc, meta, (L, L), "weak"
+        return SimpleNamespace(step=step, n=n, nbytes=nbytes, batches=batches, plan=plan,
+                               desc=desc, meta=meta, shape=(L, L), scaling="weak")
     if args.config in ("slots", "zslots"):
         # netmap RX ring drained into one ragged batch: one IP packet per
         # 2048-B slot at +14 (eth.h:44-48); slots = fixed --len + 28 B,
@@ -268,7 +323,7 @@ def make_workload(args, dev, rank, world):
 
         wc.cksum_ragged(buf, d_off, d_len, out=out, kind=kind)  # validates the layout once
 
-        def step():
+        def step(i=0):
             if fused:
                 wc.cksum_ip_udp_ragged(buf, d_off, d_len, check=False, out_hdr=out_hdr, out=out)
             else:
@@ -286,13 +341,15 @@ def make_workload(args, dev, rank, world):
                     "slot_bytes": slot, "layout": "ragged", "kind": kind}
         if fused:
             desc += ", fused IPv4 header + payload_cksum pass"
-            meta["out_hdr"] = out_hdr
         path = "grouped path" if args.config == "slots" and not fused else "gathered-stream path"
         plan = {"kernel": f"seg ({path} for these tiles)",
                 "rows_per_group": int(os.environ.get(
                     "WC_GRP_ROWS" if args.config == "slots" else "WC_SEG_ROWS", "4")),
                 "grid": int((n + 255) // 256)}
-        return step, n, nbytes, buf, out, plan, desc, meta, (offs, lens), "weak"
+        return SimpleNamespace(step=step, n=n, nbytes=nbytes,
+                               batches=[{"buf": buf, "out": out, "out_hdr": out_hdr}],
+                               plan=plan, desc=desc, meta=meta, shape=(offs, lens),
+                               scaling="weak")
     # C4: Zipf(1) lengths 64..1472 B, packed with no padding (unaligned starts)
     n = 1 << 24 if args.packets == (1 << 20) else args.packets
     lens = synth.zipf_lengths(n, seed=synth.ZIPF_SEED + rank)
@@ -309,7 +366,7 @@ def make_workload(args, dev, rank, world):
 
     wc.cksum_ragged(buf, d_off, d_len, out=out, kind=kind)  # validates the layout once
 
-    def step():
+    def step(i=0):
         if fused:
             wc.cksum_ip_udp_ragged(buf, d_off, d_len, check=False, out_hdr=out_hdr, out=out)
         else:
@@ -320,7 +377,6 @@ def make_workload(args, dev, rank, world):
             "layout": "ragged", "kind": kind}
     if fused:
         desc += ", fused IPv4 header + payload_cksum pass"
-        meta["out_hdr"] = out_hdr
     seg = int(os.environ.get("WC_SEG", "1"))
     if seg != 0:
         plan = {"kernel": "seg (segmented prefix over dense 64-packet tiles, flat fallback)",
@@ -330,7 +386,72 @@ def make_workload(args, dev, rank, world):
         plan = {"kernel": "flat (chunk-balanced, 64-packet tiles)",
                 "rows_per_group": int(os.environ.get("WC_FLAT_UN", "2")),
                 "grid": int((n + 255) // 256)}
-    return step, n, nbytes, buf, out, plan, desc, meta, (offs, lens), "weak"
+    return SimpleNamespace(step=step, n=n, nbytes=nbytes,
+                           batches=[{"buf": buf, "out": out, "out_hdr": out_hdr}],
+                           plan=plan, desc=desc, meta=meta, shape=(offs, lens), scaling="weak")
+
+
+class Timer:
+    """The timed launches of one workload on torch's current stream (the
+    stream every wc_* launch goes to), as plain launches or replayed from one
+    captured hipGraph of `per_graph` consecutive steps (a whole number of
+    rotations) -- the graph takes the Python launch cost out of small-batch
+    timings (a 64-B C3 kernel is ~9 us, a Python launch about as long)."""
+
+    def __init__(self, W, dev, use_graph: bool, rotate: int = 1, min_graph_steps: int = 8):
+        self.W, self.dev = W, dev
+        self.graph = None
+        self.per_graph = 1
+        if use_graph:
+            K = max(1, rotate)
+            self.per_graph = K * max(1, -(-min_graph_steps // K))
+            torch.cuda.synchronize(dev)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for i in range(self.per_graph):
+                    W.step(i)
+            torch.cuda.synchronize(dev)
+            self.graph = g
+
+    def rounded(self, steps: int) -> int:
+        """Steps actually timed: a whole number of graph replays."""
+        return max(1, -(-steps // self.per_graph)) * self.per_graph
+
+    def run(self, steps: int, start: int = 0) -> None:
+        if self.graph is not None:
+            for _ in range(self.rounded(steps) // self.per_graph):
+                self.graph.replay()
+        else:
+            for i in range(steps):
+                self.W.step(start + i)
+
+    def warm(self, steps: int, seconds: float) -> None:
+        t_w = time.perf_counter()
+        done = 0
+        while done < steps or time.perf_counter() - t_w < seconds:
+            self.run(self.per_graph, done)
+            done += self.per_graph
+            if done % 16 < self.per_graph:
+                torch.cuda.synchronize(self.dev)
+        torch.cuda.synchronize(self.dev)
+
+    def kernel_ms(self, steps: int) -> float:
+        """Average launch duration over `steps` (HIP events on the launch
+        stream, one bracket around all of them)."""
+        steps = self.rounded(steps)
+        stream = torch.cuda.current_stream(self.dev)
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev0.record(stream)
+        self.run(steps)
+        ev1.record(stream)
+        ev1.synchronize()
+        return ev0.elapsed_time(ev1) / steps
+
+    def steps_for(self, seconds: float) -> int:
+        """Steps that take about `seconds` (from one short calibration)."""
+        ms = self.kernel_ms(self.per_graph)
+        return self.rounded(max(self.per_graph, int(seconds * 1e3 / max(ms, 1e-3))))
 
 
 def cpu_threads(args):
@@ -422,18 +543,19 @@ def last_count(args):
     return share - (share - 1) // win * win
 
 
-def parity_check(args, buf, out, shape, nbytes, meta=None):
-    """Bit-exact check of the last step's results over EVERY packet of the
-    batch against the oracle (run outside the timed region)."""
+def parity_batch(args, b, shape):
+    """Bit-exact check of one batch's last results over EVERY packet against
+    the oracle (run outside the timed region): (checked, mismatches, extra)."""
     from oracle import c_oracle
+    buf, out, out_hdr = b["buf"], b["out"], b.get("out_hdr")
     k = 1 if args.kind == "payload" else 0
     if args.config in ("rx", "zrx"):
         offs, flens = shape
         hb = buf[: int(offs[-1]) + int(flens[-1])].cpu().numpy()
         want = c_oracle.rx_verdict_ragged(hb, offs, flens)
         got = out.cpu().numpy()
-        return {"checked_packets": int(got.size), "mismatches": int((got != want).sum()),
-                "verdicts_ok": int(np.isin(want, (0, 1)).sum())}
+        return int(got.size), int((got != want).sum()), {
+            "verdicts_ok": int(np.isin(want, (0, 1)).sum())}
     got = out.cpu().numpy().view(np.uint16)
     if args.config in ("c2", "c3", "c5"):
         hb = buf[: got.size * shape[1]].cpu().numpy()
@@ -452,15 +574,28 @@ def parity_check(args, buf, out, shape, nbytes, meta=None):
         offs, lens = shape
         want = c_oracle.cksum_ragged(hb, offs, lens, kind=k)
     bad = int((got != want).sum())
-    if meta is not None and meta.get("out_hdr") is not None:
+    if out_hdr is not None:
         # fused pass: the IPv4 header checksums too (ip_cksum(ip, hl), 0 for IPv6)
         b0 = hb[offs.astype(np.int64)]
         v4 = (b0 >> 4) == 4
         hl = np.where(v4, (b0 & 0x0F).astype(np.uint16) * 4, 0).astype(np.uint16)
         want_h = np.where(v4, c_oracle.cksum_ragged(hb, offs, hl, kind=0), 0).astype(np.uint16)
-        got_h = meta["out_hdr"].cpu().numpy().view(np.uint16)[: got.size]
+        got_h = out_hdr.cpu().numpy().view(np.uint16)[: got.size]
         bad += int((got_h != want_h).sum())
-    return {"checked_packets": int(got.size), "mismatches": bad}
+    return int(got.size), bad, {}
+
+
+def parity_check(args, W):
+    """Every packet of every batch of W against the oracle."""
+    checked = bad = 0
+    extra = {}
+    for b in W.batches:
+        c, m, e = parity_batch(args, b, W.shape)
+        checked += c
+        bad += m
+        for key, v in e.items():
+            extra[key] = extra.get(key, 0) + v
+    return {"checked_packets": checked, "mismatches": bad, **extra}
 
 
 def c5_leg(args, dev, rank, world, coll_dev):
@@ -533,6 +668,95 @@ def c5_leg(args, dev, rank, world, coll_dev):
     }
 
 
+def traffic_entry(args, meta, path):
+    """HBM bytes per launch for this workload from profiles/traffic.json
+    (PMC FETCH_SIZE x2 + WRITE_SIZE, separate rocprofv3 passes): (bytes,
+    source) or (None, None)."""
+    try:
+        tf = json.loads(Path(path).read_text())
+    except (OSError, ValueError):
+        return None, None
+    key = f"{args.config}:{meta.get('packet_bytes', 'zipf')}"
+    if args.kind != "ip" and args.config not in ("rx", "zrx"):
+        key += f":{args.kind}"
+    if args.headers and args.config not in ("rx", "zrx"):
+        key += ":headers"
+    if args.fused:
+        key += ":fused"
+    if key not in tf:
+        return None, None
+    e = tf[key]
+    return e["hbm_bytes_per_launch"], (
+        f"{os.path.relpath(path, ROOT)} [{key}] ({e.get('round', 'r01')}: rocprofv3 --pmc "
+        f"FETCH_SIZE x2 + WRITE_SIZE, separate passes; a static lookup, not this run)")
+
+
+def measure_leg(args, dev, rank, world, coll_dev, sub, use_graph):
+    """One secondary measurement (c3 size, c4, C2 rotating): build the
+    workload `sub` (args with its config), warm it, time it on HIP events,
+    check every packet of every batch; frees its buffers.  At K > 1 rotating
+    batches it also times batch 0 alone (frac_l3_resident)."""
+    from warpcore_amd import dist as wdist
+    W = make_workload(sub, dev, rank, world)
+    K = len(W.batches)
+    T = Timer(W, dev, use_graph, rotate=K)
+    T.warm(2 * T.per_graph, 0.2)
+    steps = T.steps_for(args.extra_seconds)
+    wdist.barrier(dev)
+    ms = wdist.max_over_ranks(T.kernel_ms(steps), coll_dev)
+    res = {"kernel_ms_avg_max_rank": round(ms, 5),
+           "GBps": round(W.nbytes / (ms * 1e-3) / 1e9, 1),
+           "frac": round(W.nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+           "batches": K, "footprint_GB": round(K * W.nbytes / 1e9, 3),
+           "steps": steps, "launch": "hipGraph replay" if T.graph is not None else "stream"}
+    par = parity_check(sub, W)  # every batch's results are from its last timed launch
+    res["parity"] = {"checked_packets": wdist.sum_over_ranks(par["checked_packets"], coll_dev),
+                     "mismatches": wdist.sum_over_ranks(par["mismatches"], coll_dev)}
+    if K > 1:
+        one = SimpleNamespace(**vars(W))
+        one.batches = W.batches[:1]
+        T1 = Timer(one, dev, use_graph, rotate=1)
+        T1.warm(T1.per_graph, 0.05)
+        wdist.barrier(dev)
+        ms1 = wdist.max_over_ranks(T1.kernel_ms(T1.steps_for(args.extra_seconds)), coll_dev)
+        res["frac_l3_resident"] = round(W.nbytes / (ms1 * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+        res["kernel_ms_l3_resident"] = round(ms1, 5)
+        del T1, one
+    tb, _ = traffic_entry(sub, W.meta, args.traffic_file)
+    res["traffic_over_algorithmic"] = round(tb / W.nbytes, 4) if tb else None
+    res["kernel"] = W.plan.get("kernel")
+    del T, W
+    torch.cuda.synchronize(dev)
+    torch.cuda.empty_cache()
+    return res
+
+
+def extra_legs(args, dev, rank, world, coll_dev):
+    """The default line's secondary configs, each timed on the device like
+    the headline (after it): C2 over 4 rotating batches, BASELINE configs[2]
+    (c3) on rotating batches and configs[3] (c4)."""
+    base = copy.copy(args)
+    base.kind, base.headers, base.fused, base.batches = "ip", False, False, 0
+    rot = copy.copy(base)
+    rot.config, rot.packets, rot.batches = "c2", args.packets, 4
+    c2rot = measure_leg(args, dev, rank, world, coll_dev, rot, use_graph=False)
+    c3 = {"workload": (f"BASELINE configs[2]: {args.c3_packets} packets x each size, stride = "
+                       f"size, ip_cksum; steps rotate over K = ceil({args.rotate_bytes} B / "
+                       f"batch) distinct seeded batches (HBM rate: frac); the single batch "
+                       f"re-read (frac_l3_resident) where K > 1"),
+          "sizes": {}}
+    for L in C3_SIZES:
+        sub = copy.copy(base)
+        sub.config, sub.len, sub.packets = "c3", L, args.c3_packets
+        c3["sizes"][str(L)] = measure_leg(args, dev, rank, world, coll_dev, sub, use_graph=True)
+    sub = copy.copy(base)
+    sub.config, sub.packets = "c4", args.c4_packets
+    c4 = measure_leg(args, dev, rank, world, coll_dev, sub, use_graph=True)
+    c4["workload"] = (f"BASELINE configs[3]: {args.c4_packets} packets, Zipf(s=1) lengths "
+                      f"64-1472 B, packed (unaligned starts), ip_cksum")
+    return c2rot, c3, c4
+
+
 def main():
     args = parse()
     how, n_ranks = resolve_launch(args)
@@ -546,33 +770,29 @@ def main():
     if args.fused:  # the fused pass is payload_cksum over real UDP headers
         args.kind, args.headers = "payload", True
 
-    step, n, nbytes, buf, out, plan, desc, meta, shape, scaling = make_workload(
-        args, dev, rank, world)
-
-    t_w = time.perf_counter()
-    done = 0
-    while done < args.warmup or time.perf_counter() - t_w < args.warmup_seconds:
-        step()
-        done += 1
-        if done % 16 == 0:
-            torch.cuda.synchronize(dev)
+    W = make_workload(args, dev, rank, world)
+    n, nbytes, meta = W.n, W.nbytes, W.meta
+    K = len(W.batches)
+    use_graph = args.graph == "on" or (args.graph == "auto" and args.config == "c3")
+    T = Timer(W, dev, use_graph, rotate=K)
+    T.warm(args.warmup, args.warmup_seconds)
     wdist.barrier(dev)
 
+    steps = T.rounded(args.steps)
     stream = torch.cuda.current_stream(dev)  # the stream every launch goes to
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
-    for _ in range(args.steps):
-        step()
+    T.run(steps)
     ev1.record(stream)
     wdist.barrier(dev)
     elapsed = time.perf_counter() - t0
-    kernel_ms = ev0.elapsed_time(ev1) / args.steps
+    kernel_ms = ev0.elapsed_time(ev1) / steps
 
     elapsed = wdist.max_over_ranks(elapsed, coll_dev)
     kernel_ms_max = wdist.max_over_ranks(kernel_ms, coll_dev)
-    total_bytes = float(wdist.sum_over_ranks(int(nbytes), coll_dev)) * args.steps
+    total_bytes = float(wdist.sum_over_ranks(int(nbytes), coll_dev)) * steps
     value = total_bytes / elapsed / GIB
     # Roofline of the dominant kernel: one rank's algorithmic bytes per launch
     # over the slowest rank's average launch time (all ranks move the same
@@ -580,8 +800,20 @@ def main():
     achieved = nbytes / (kernel_ms_max * 1e-3) / 1e9
     frac_job = value * GIB / 1e9 / (world * HBM_PEAK_GBPS)
 
-    parity = parity_check(args, buf, out, shape, nbytes, meta)
-    meta.pop("out_hdr", None)
+    # Single-buffer figure beside a rotating run (the Infinity-Cache-resident
+    # rate the rotation avoids).
+    frac_l3 = None
+    if K > 1:
+        one = SimpleNamespace(**vars(W))
+        one.batches = W.batches[:1]
+        T1 = Timer(one, dev, use_graph, rotate=1)
+        T1.warm(T1.per_graph, 0.1)
+        wdist.barrier(dev)
+        ms1 = wdist.max_over_ranks(T1.kernel_ms(steps), coll_dev)
+        frac_l3 = round(nbytes / (ms1 * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+        del T1, one
+
+    parity = parity_check(args, W)
     for key in list(parity):
         if isinstance(parity[key], int):
             parity[key] = wdist.sum_over_ranks(parity[key], coll_dev)
@@ -589,6 +821,7 @@ def main():
     # after the timed region the ranks exchange their 2-byte
     # results (RCCL all-gather over xGMI; host tensors for the gloo
     # rehearsal), so every rank holds the whole job's results in packet order.
+    out = W.batches[0]["out"]
     gather = None
     if (world > 1 or wdist._pg_active()) and out.numel() == n and out.element_size() == 2:
         src = out.view(torch.int16)
@@ -606,46 +839,48 @@ def main():
                   "ms": round(wdist.max_over_ranks(g_ms, coll_dev), 3),
                   "ranks_mismatched": wdist.sum_over_ranks(bad, coll_dev)}
 
-    traffic = None
-    traffic_source = None
-    try:
-        tf = json.loads(Path(args.traffic_file).read_text())
-        key = f"{args.config}:{meta.get('packet_bytes', 'zipf')}"
-        if args.kind != "ip" and args.config not in ("rx", "zrx"):
-            key += f":{args.kind}"
-        if args.headers and args.config not in ("rx", "zrx"):
-            key += ":headers"
-        if args.fused:
-            key += ":fused"
-        if key in tf:
-            traffic = tf[key]["hbm_bytes_per_launch"]
-            traffic_source = (f"{os.path.relpath(args.traffic_file, ROOT)} [{key}] "
-                              f"({tf[key].get('round', 'r01')}: rocprofv3 --pmc FETCH_SIZE x2 + "
-                              f"WRITE_SIZE, separate passes; a static lookup, not this run)")
-    except (OSError, ValueError, KeyError):
-        traffic = None
+    traffic, traffic_source = traffic_entry(args, meta, args.traffic_file)
 
     # The CPU baseline at every N (rank 0's host cores, its own batch), then
-    # the C5 strong-scaling leg -- both after the headline's timed region.
+    # the secondary legs and the C5 strong-scaling leg -- all after the
+    # headline's timed region.
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args, buf, shape, nbytes)
+        cpu = cpu_baseline(args, W.batches[0]["buf"], W.shape, nbytes)
     wdist.barrier(dev)
+    plan, desc, scaling = W.plan, W.desc, W.scaling
+    del T, W, out
+    torch.cuda.synchronize(dev)
+    torch.cuda.empty_cache()
+    c2rot = c3 = c4 = None
+    if not args.no_extra and args.config == "c2" and not args.fused and args.kind == "ip":
+        c2rot, c3, c4 = extra_legs(args, dev, rank, world, coll_dev)
     c5 = None
     if not args.no_c5 and args.config != "c5":
-        del step, buf, out
-        torch.cuda.empty_cache()
         c5 = c5_leg(args, dev, rank, world, coll_dev)
 
     if rank == 0:
+        roof = {"bound": "hbm", "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                "traffic": traffic, "traffic_source": traffic_source,
+                "frac_job": round(frac_job, 4),
+                "kernel_ms_avg": round(kernel_ms, 5),
+                "kernel_ms_avg_max_rank": round(kernel_ms_max, 5),
+                "timing": "hipGraph replay" if use_graph else "stream launches"}
+        if frac_l3 is not None:
+            roof["frac_l3_resident"] = frac_l3
+        if c2rot is not None:
+            roof["frac_rotating"] = c2rot["frac"]
+            roof["rotating"] = c2rot
         line = {
             "metric": METRIC,
             "value": round(value, 2),
             "unit": "GiB/s",
             "n_gpus": world,
-            "steps": args.steps,
+            "steps": steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "ms_per_step": round(elapsed / steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": scaling,
             "vs_baseline": None,
@@ -657,17 +892,14 @@ def main():
                        if args.config in ("rx", "zrx") else ""),
             "config": {"workload": desc, **meta, "parallelism": f"packet-shard x{world}",
                        "kernel_shape": plan, "payload_GBps": round(value * GIB / 1e9, 1)},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1),
-                         "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                         "traffic": traffic, "traffic_source": traffic_source,
-                         "frac_job": round(frac_job, 4),
-                         "kernel_ms_avg": round(kernel_ms, 5),
-                         "kernel_ms_avg_max_rank": round(kernel_ms_max, 5)},
+            "roofline": roof,
             "cpu_baseline": cpu,
             "parity": parity,
             "c5": c5,
         }
+        if c3 is not None:
+            line["c3"] = c3
+            line["c4"] = c4
         if gather is not None:
             line["results_allgather"] = gather
         print(json.dumps(line), flush=True)

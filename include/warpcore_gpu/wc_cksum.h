@@ -147,7 +147,11 @@ int wc_cksum_host(const void *h_base, uint64_t h_bytes, const uint64_t *h_off,
 
 /* Page-lock a host region (e.g. the netmap buffer area w->mem,
  * backend_netmap.c:149-151) so wc_cksum_host can DMA from it directly.
- * Registering the same base again is a no-op (a larger size re-registers). */
+ * Registering the same base again drops the old registration and pins the
+ * pages mapped there now, at the new size (if that fails, the old range is
+ * pinned again and the error returned).  Call wc_host_unregister before
+ * freeing a registered region: a batch over a freed and re-allocated range
+ * that was not registered again reads the pages pinned before the free. */
 int wc_host_register(void *h_ptr, uint64_t bytes);
 int wc_host_unregister(void *h_ptr);
 

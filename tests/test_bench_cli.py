@@ -64,3 +64,21 @@ def test_cpu_baseline_threads(monkeypatch):
         th, vis, why = bench.cpu_threads(_args(1))
         assert (th, vis) == (1, visible) and "OMP_NUM_THREADS" in why
     assert bench.cpu_threads(_args(1, cpu_threads=3))[0] == 3
+
+
+@pytest.mark.parametrize("batch,want", [(64 << 20, 16), (1 << 30, 1), (1543503872, 1),
+                                        (268435456, 4), (134217728, 8), (9000 << 20, 1),
+                                        ((1 << 30) - 1, 2)])
+def test_rotation_covers_the_infinity_cache(batch, want):
+    """Strided batches rotate over ceil(1 GiB / batch) distinct batches, so
+    the footprint is >= 4x the 256 MiB Infinity Cache (C3 64 B: 16 x 67 MB;
+    C2's 1.54 GB batch: 1)."""
+    a = bench.parse([])
+    assert bench.rotation(batch, a) == want
+    assert bench.rotation(batch, bench.parse(["--batches", "4"])) == 4
+
+
+def test_default_line_carries_the_secondary_legs():
+    a = bench.parse([])
+    assert not a.no_extra and a.c3_packets == 1 << 20 and a.c4_packets == 1 << 24
+    assert bench.C3_SIZES == (64, 256, 576, 1472, 9000)

@@ -26,11 +26,16 @@ def _last_json(out: str) -> dict:
 SMALL_C5 = ["--total-packets", str(1 << 22), "--window-packets", str(1 << 20)]
 
 
+SMALL_EXTRA = ["--c3-packets", "65536", "--c4-packets", "200000", "--rotate-bytes",
+               str(64 << 20), "--extra-seconds", "0.05"]
+
+
 def test_bench_one_gpu_line(gpu):
-    """The driver's line at reduced size: C2 headline, CPU baseline and the C5
-    strong-scaling leg (2^22 packets over a 2^20 window here)."""
+    """The driver's line at reduced size: C2 headline, CPU baseline, the C5
+    strong-scaling leg (2^22 packets over a 2^20 window here) and the c3 / c4
+    objects and C2 rotating cross-check (rotating over >= 64 MiB here)."""
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--steps", "5", "--warmup", "1",
-                        "--packets", "65536", "--cpu-seconds", "0.5", *SMALL_C5],
+                        "--packets", "65536", "--cpu-seconds", "0.5", *SMALL_C5, *SMALL_EXTRA],
                        capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     line = _last_json(r.stdout)
@@ -44,6 +49,37 @@ def test_bench_one_gpu_line(gpu):
     assert "4 launch(es)" in c5["workload"] and 0 < c5["frac_job"] < 1.5
     assert c5["parity"] == {"checked_packets": 3 << 16, "mismatches": 0,
                             "sample": c5["parity"]["sample"]}
+    # c3: every size, rotating over ceil(64 MiB / batch) batches, all checked
+    c3 = line["c3"]["sizes"]
+    assert sorted(int(k) for k in c3) == [64, 256, 576, 1472, 9000]
+    for L, e in c3.items():
+        K = -(-(64 << 20) // (65536 * int(L)))
+        assert e["batches"] == K, (L, e)
+        assert e["parity"] == {"checked_packets": K * 65536, "mismatches": 0}, (L, e)
+        assert 0 < e["frac"] < 1.5
+        assert ("frac_l3_resident" in e) == (K > 1)
+    c4 = line["c4"]
+    assert c4["parity"] == {"checked_packets": 200000, "mismatches": 0} and c4["frac"] > 0
+    rot = line["roofline"]["rotating"]
+    assert rot["batches"] == 4 and rot["parity"] == {"checked_packets": 4 * 65536,
+                                                      "mismatches": 0}
+    assert line["roofline"]["frac_rotating"] == rot["frac"]
+
+
+def test_bench_c3_rotating_line(gpu):
+    """`--config c3` rotates over distinct batches (HBM, not the Infinity
+    Cache), replays its launches from a hipGraph, checks every batch and
+    reports the single-buffer rate beside it."""
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--config", "c3", "--len", "64",
+                        "--steps", "20", "--warmup", "2", "--packets", "65536",
+                        "--rotate-bytes", str(16 << 20), "--no-c5", "--no-cpu-baseline"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = _last_json(r.stdout)
+    assert line["config"]["batches"] == 4 and line["steps"] % 8 == 0
+    assert line["parity"] == {"checked_packets": 4 * 65536, "mismatches": 0}
+    assert line["roofline"]["timing"] == "hipGraph replay"
+    assert 0 < line["roofline"]["frac_l3_resident"] < 1.5
 
 
 def test_bench_two_ranks_rehearsal(gpu):
@@ -56,7 +92,7 @@ def test_bench_two_ranks_rehearsal(gpu):
                         "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
                         "--master-port", str(port), str(ROOT / "bench.py"), "--gpus", "2",
                         "--steps", "5", "--warmup", "1", "--packets", "65536",
-                        "--cpu-seconds", "0.3", *SMALL_C5],
+                        "--cpu-seconds", "0.3", *SMALL_C5, *SMALL_EXTRA],
                        capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     line = _last_json(r.stdout)
@@ -68,6 +104,8 @@ def test_bench_two_ranks_rehearsal(gpu):
     assert line["parity"] == {"checked_packets": 2 * 65536, "mismatches": 0}
     assert line["results_allgather"]["ranks_mismatched"] == 0
     assert line["results_allgather"]["bytes_per_rank"] == 2 * 65536
+    assert line["c3"]["sizes"]["64"]["parity"]["mismatches"] == 0
+    assert line["c4"]["parity"] == {"checked_packets": 2 * 200000, "mismatches": 0}
 
 
 @pytest.mark.parametrize("args", [["--config", "c4", "--packets", "200000"],
@@ -85,7 +123,7 @@ def test_bench_other_configs(gpu, args):
     """The secondary bench lines (C4, payload_cksum, the netmap RX-ring layout)
     stay runnable and bit-exact."""
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--steps", "3", "--warmup", "1",
-                        "--cpu-seconds", "0.2", "--no-c5", *args],
+                        "--cpu-seconds", "0.2", "--no-c5", "--no-extra", *args],
                        capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     line = _last_json(r.stdout)
@@ -101,7 +139,7 @@ def test_bench_spawns_ranks_without_torchrun(gpu):
     env["WC_DIST_BACKEND"] = "gloo"
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2",
                         "--steps", "5", "--warmup", "1", "--packets", "65536", "--no-c5",
-                        "--no-cpu-baseline"],
+                        "--no-cpu-baseline", "--no-extra"],
                        capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     line = _last_json(r.stdout)
@@ -158,7 +196,7 @@ def test_bench_rccl_code_path_one_rank(gpu):
                MASTER_PORT=str(port), WC_DIST_FORCE_PG="1", WC_DIST_BACKEND="nccl")
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "1", "--steps", "5",
                         "--warmup", "1", "--packets", "65536", "--no-cpu-baseline",
-                        *SMALL_C5],
+                        "--no-extra", *SMALL_C5],
                        capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     line = _last_json(r.stdout)

@@ -764,6 +764,51 @@ def test_host_zero_copy_small_batches(gpu, kind, n):
     np.testing.assert_array_equal(got, want)
 
 
+def test_host_register_after_free_and_reuse(gpu):
+    """register -> free without unregister -> a new buffer mapped at the same
+    address -> register again: the zero-copy path must read the NEW pages
+    (the library re-pins on every register of a base), and a re-register of
+    a live region at a larger size keeps working."""
+    import ctypes
+    import ctypes.util
+    libc = ctypes.CDLL(ctypes.util.find_library("c"), use_errno=True)
+    libc.mmap.restype = ctypes.c_void_p
+    libc.mmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                          ctypes.c_int, ctypes.c_long]
+    libc.munmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    PROT_RW, MAP_PRIV_ANON, MAP_FIXED = 0x3, 0x22, 0x10
+    size, slot, n = 1 << 20, 2048, 256
+    addr = libc.mmap(None, size, PROT_RW, MAP_PRIV_ANON, -1, 0)
+    assert addr not in (None, ctypes.c_void_p(-1).value)
+    rng = np.random.default_rng(77)
+    offs = (np.arange(n, dtype=np.uint64) * slot + 3).astype(np.uint64)
+    lens = rng.integers(1, slot - 8, n).astype(np.uint16)
+    try:
+        a1 = np.ctypeslib.as_array((ctypes.c_uint8 * size).from_address(addr))
+        a1[:] = rng.integers(0, 256, size, dtype=np.uint8)
+        wc.host_register(a1)
+        np.testing.assert_array_equal(wc.cksum_host(a1, offs, lens),
+                                      c_oracle.cksum_ragged(a1, offs, lens))
+        # freed without wc_host_unregister; new pages mapped at the same address
+        assert libc.munmap(addr, size) == 0
+        got_addr = libc.mmap(addr, size, PROT_RW, MAP_PRIV_ANON | MAP_FIXED, -1, 0)
+        assert got_addr == addr
+        a2 = np.ctypeslib.as_array((ctypes.c_uint8 * size).from_address(addr))
+        a2[:] = rng.integers(0, 256, size, dtype=np.uint8)
+        wc.host_register(a2)
+        want2 = c_oracle.cksum_ragged(a2, offs, lens)
+        np.testing.assert_array_equal(wc.cksum_host(a2, offs, lens), want2)
+        # same base, smaller then larger size: still registered, still exact
+        wc.host_register(a2[: size // 2])
+        np.testing.assert_array_equal(wc.cksum_host(a2, offs, lens), want2)
+        wc.host_register(a2)
+        np.testing.assert_array_equal(wc.cksum_host(a2, offs, lens), want2)
+        wc.host_unregister(a2)
+        np.testing.assert_array_equal(wc.cksum_host(a2, offs, lens), want2)  # pipelined now
+    finally:
+        libc.munmap(addr, size)
+
+
 @pytest.mark.parametrize("kind", ["ip", "payload"])
 def test_host_path_unordered_gather(gpu, kind):
     """Offsets in random order through the pipelined path (gathered into

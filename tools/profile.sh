@@ -11,7 +11,7 @@ TAG=${TAG:-r01}
 OUT=$REPO/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-ARGS=${BENCH_ARGS:---steps 50 --warmup 5 --no-cpu-baseline}
+ARGS=${BENCH_ARGS:---steps 50 --warmup 5 --no-cpu-baseline --no-c5 --no-extra}
 
 run() {  # $1 = name, rest = rocprofv3 options
     local name=$1; shift

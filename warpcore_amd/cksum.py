@@ -335,8 +335,9 @@ def rx_verdict_ragged(base: torch.Tensor, offsets: torch.Tensor, frame_lens: tor
         raise ValueError(f"out must be a contiguous 1-byte tensor of >= n entries on {base.device}")
     if drops is None:
         drops = torch.zeros(1, dtype=torch.int64, device=base.device)
-    elif drops.numel() < 1 or drops.element_size() != 8 or drops.device != base.device:
-        raise ValueError("drops must be an 8-byte device tensor (accumulated)")
+    elif (drops.numel() < 1 or drops.dtype not in (torch.int64, torch.uint64)
+          or not drops.is_contiguous() or drops.device != base.device):
+        raise ValueError("drops must be a contiguous int64 / uint64 device tensor (accumulated)")
     with _on_device(base.device):
         _check("wc_rx_verdict_ragged", _lib.load().wc_rx_verdict_ragged(
             _dev_ptr(base), _dev_ptr(offsets), _dev_ptr(frame_lens), n, out.data_ptr(),
@@ -391,12 +392,29 @@ def cksum_host(buf: np.ndarray, offsets: np.ndarray, lengths: np.ndarray,
     return out
 
 
+# Buffers page-locked through host_register, by base address: the library
+# pins the pages mapped at that address, so the array is kept alive here until
+# host_unregister (a buffer garbage-collected while registered could give its
+# address to a new one that the old pinned pages do not back).
+_registered: dict = {}
+
+
 def host_register(buf: np.ndarray) -> None:
+    """Page-lock `buf` for the zero-copy / direct-DMA host path.  The array
+    is held until host_unregister(buf); registering it (or a new array at the
+    same address) again re-pins the pages mapped there now."""
+    if not isinstance(buf, np.ndarray) or not buf.flags["C_CONTIGUOUS"]:
+        raise ValueError("host_register needs a C-contiguous numpy array")
     _check("wc_host_register", _lib.load().wc_host_register(buf.ctypes.data, buf.nbytes))
+    _registered[buf.ctypes.data] = buf
 
 
 def host_unregister(buf: np.ndarray) -> None:
-    _check("wc_host_unregister", _lib.load().wc_host_unregister(buf.ctypes.data))
+    addr = buf.ctypes.data
+    try:
+        _check("wc_host_unregister", _lib.load().wc_host_unregister(addr))
+    finally:
+        _registered.pop(addr, None)
 
 
 # --------------------------------------------------------------------------

@@ -298,7 +298,7 @@ wc::Shape shape_for_chunks(uint32_t nch, bool full, bool payload, bool aligned,
     if (sparse && payload && nch <= 16)
         return {8, 2, 4};
     // 9..24 chunks: 8 lanes x 3 chunks, two packets per group -- fewer dead
-    // lane slots than 16 x 2 (tools/sweep_mid.sh: 256 B 78.7 -> 84.1 %,
+    // lane slots than 16 x 2 (profiles/sweep_r01_mid_shapes.log: 256 B 78.7 -> 84.1 %,
     // 200 B 55 -> 67.5 %, 256 B at +14 50 -> 60 % of HBM peak)
     if (nch <= 16 || (nch <= 24 && !full))
         return {8, 3, 2};
@@ -1192,32 +1192,44 @@ int wc_host_register(void *h_ptr, uint64_t bytes)
     int rc = init_locked(-1, &D);
     if (rc)
         return rc;
-    // Registering a region again is a no-op (it stays registered across
-    // wc_gpu_fini); a larger size re-registers it.
+    // Registering a base address again always pins the pages mapped there
+    // NOW: the caller may have freed the old region without
+    // wc_host_unregister and got a new buffer at the same address, whose
+    // pages the old registration (and its cached device addresses) do not
+    // cover.  So the old registration is dropped and the range registered
+    // afresh; if that fails, the old range is registered again so a live
+    // region keeps working, and the error is returned.
+    uint64_t old_bytes = 0;
     auto it = g_registered.find((uintptr_t)h_ptr);
     if (it != g_registered.end()) {
-        if (it->second.bytes >= bytes)
-            return WC_OK;
+        old_bytes = it->second.bytes;
         g_registered.erase(it);
         (void)hipHostUnregister(h_ptr);
     }
-    // Portable: every device (wc_cksum_host_multi's shards) may DMA from it.
-    hipError_t e = hipHostRegister(h_ptr, bytes, hipHostRegisterMapped | hipHostRegisterPortable);
-    if (e != hipSuccess)
-        return hip_err(e);
-    void *dptr = nullptr;
-    e = hipHostGetDevicePointer(&dptr, h_ptr, 0);
-    if (e != hipSuccess) {
-        (void)hipHostUnregister(h_ptr);
-        return hip_err(e);
-    }
-    Registration reg;
-    reg.bytes = bytes;
-    int dev = 0;
-    if (current_device(&dev) == WC_OK)
-        reg.dptr[dev] = (const uint8_t *)dptr;
-    g_registered[(uintptr_t)h_ptr] = reg;
-    return WC_OK;
+    const unsigned flags = hipHostRegisterMapped | hipHostRegisterPortable;
+    auto pin = [&](uint64_t nb) -> hipError_t {
+        // Portable: every device (wc_cksum_host_multi's shards) may DMA from it.
+        hipError_t e = hipHostRegister(h_ptr, nb, flags);
+        if (e != hipSuccess)
+            return e;
+        void *dptr = nullptr;
+        e = hipHostGetDevicePointer(&dptr, h_ptr, 0);
+        if (e != hipSuccess) {
+            (void)hipHostUnregister(h_ptr);
+            return e;
+        }
+        Registration reg;
+        reg.bytes = nb;
+        int dev = 0;
+        if (current_device(&dev) == WC_OK)
+            reg.dptr[dev] = (const uint8_t *)dptr;
+        g_registered[(uintptr_t)h_ptr] = reg;
+        return hipSuccess;
+    };
+    const hipError_t e = pin(bytes);
+    if (e != hipSuccess && old_bytes)
+        (void)pin(old_bytes);
+    return hip_err(e);
 }
 
 int wc_host_unregister(void *h_ptr)
