@@ -37,6 +37,24 @@ def slot_ring(frames, slot: int = 2048, rng=None, pad: int = 64):
     return buf, offs, lens
 
 
+RX_MODES = {"default": {}, "rows2": {"WC_RX_ROWS": "2"}, "early": {"WC_RX_EARLY": "1"},
+            "rows2_early": {"WC_RX_ROWS": "2", "WC_RX_EARLY": "1"}}
+
+
+@pytest.fixture(params=list(RX_MODES))
+def rx_mode(request, monkeypatch, gpu):
+    """Every kernel mode of wc_rx_verdict_* (WC_RX_ROWS, WC_RX_EARLY: 2- or
+    4-row stream groups, parse before or during the stream) must give the
+    same verdicts."""
+    for k, v in RX_MODES[request.param].items():
+        monkeypatch.setenv(k, v)
+    wc.reload_config()
+    yield request.param
+    for k in RX_MODES[request.param]:
+        monkeypatch.delenv(k)
+    wc.reload_config()
+
+
 def check(buf, offs, lens, d):
     want = c_oracle.rx_verdict_ragged(buf, offs, lens)
     t = torch.zeros(buf.size + 64, dtype=torch.uint8, device=d)
@@ -51,7 +69,7 @@ def check(buf, offs, lens, d):
 
 
 @pytest.mark.parametrize("seed", [1, 2, 3])
-def test_rx_verdict_netmap_ring(gpu, seed):
+def test_rx_verdict_netmap_ring(gpu, seed, rx_mode):
     rng = np.random.default_rng(seed)
     frames = rx_ring(rng, 30 * len(RX_CASES))
     buf, offs, lens = slot_ring(frames, rng=rng)
@@ -60,7 +78,7 @@ def test_rx_verdict_netmap_ring(gpu, seed):
 
 
 @pytest.mark.parametrize("align,lead", [(1, 0), (1, 5), (2, 14), (16, 3)])
-def test_rx_verdict_packed(gpu, align, lead):
+def test_rx_verdict_packed(gpu, align, lead, rx_mode):
     """Frames back to back at every alignment (a ring drained into one buffer)."""
     rng = np.random.default_rng(align * 10 + lead)
     frames = rx_ring(rng, 20 * len(RX_CASES))
@@ -68,7 +86,7 @@ def test_rx_verdict_packed(gpu, align, lead):
     check(buf, offs, lens, gpu)
 
 
-def test_rx_verdict_valid_ring_mtu(gpu):
+def test_rx_verdict_valid_ring_mtu(gpu, rx_mode):
     """2^16 well-formed MTU frames (IPv4 / IPv6, ~1/7 with IPv4 options) in
     2048-B slots: every verdict OK (or OK_NO_CKSUM for a computed 0), then
     flip a bit in 1000 of them: every one the oracle drops is dropped (IPv6
@@ -99,7 +117,7 @@ def test_rx_verdict_empty_and_tiny(gpu):
     assert got.numel() == 0 and int(drops.item()) == 0
 
 
-def test_rx_verdict_frames_at_buffer_end(gpu):
+def test_rx_verdict_frames_at_buffer_end(gpu, rx_mode):
     """Frames ending on the buffer's last byte, their lengths bounding every
     load (a fault here would take the GPU down, so the bound is tested)."""
     rng = np.random.default_rng(9)
@@ -114,7 +132,7 @@ def test_rx_verdict_frames_at_buffer_end(gpu):
 
 @pytest.mark.parametrize("register", [False, True])
 @pytest.mark.parametrize("n", [64, 4096, 200000])
-def test_rx_verdict_host(gpu, register, n):
+def test_rx_verdict_host(gpu, register, n, rx_mode):
     """The RX ring in host memory (netmap's w->mem): zero-copy for a small
     registered batch, the pipelined copy otherwise."""
     rng = np.random.default_rng(n + register)

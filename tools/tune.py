@@ -86,6 +86,8 @@ def main():
                     help="fused IPv4 header + payload_cksum pass (wc_cksum_ip_udp_*)")
     ap.add_argument("--headers", action="store_true",
                     help="well-formed IPv4 / IPv6 UDP headers (synth.stamp_udp_headers)")
+    ap.add_argument("--rx-arp", type=int, default=0,
+                    help="rx / zrx: every K-th frame an ARP frame (no UDP check)")
     ap.add_argument("--ragged", action="store_true",
                     help="c2/c3 through the ragged entry point (offset/length arrays)")
     args = ap.parse_args()
@@ -93,7 +95,26 @@ def main():
     dev = torch.device("cuda:0")
     wc.gpu_init(0)
     stream = torch.cuda.current_stream()
-    if args.config in ("c4", "c4r", "zslots"):
+    if args.config in ("rx", "zrx"):
+        # netmap RX ring of well-formed UDP frames (bench.py --config rx / zrx);
+        # --rx-arp K turns every K-th frame into an ARP frame (no UDP check)
+        n = args.packets if args.packets != (1 << 20) or args.config == "rx" else 1 << 21
+        ip_lens = (np.full(n, args.len + 28, dtype=np.uint16) if args.config == "rx"
+                   else synth.zipf_lengths(n))
+        buf = torch.empty(n * 2048 + 64, dtype=torch.uint8, device=dev)
+        wc.synth_fill(buf, 1, nbytes=n * 2048)
+        f_off, f_len = synth.make_rx_ring(buf, n, ip_lens)
+        if args.rx_arp:
+            sel = torch.from_numpy(f_off[::args.rx_arp].astype(np.int64)).to(dev)
+            buf[sel + 12] = 0x08
+            buf[sel + 13] = 0x06
+        d_off, d_len = torch.from_numpy(f_off).to(dev), torch.from_numpy(f_len).to(dev)
+        nbytes = int(f_len.astype(np.uint64).sum())
+        out = torch.empty(n, dtype=torch.uint8, device=dev)
+        drops = torch.zeros(1, dtype=torch.int64, device=dev)
+        run = lambda: wc.rx_verdict_ragged(buf, d_off, d_len, out=out, check=False,  # noqa: E731
+                                           drops=drops)
+    elif args.config in ("c4", "c4r", "zslots"):
         # c4: Zipf lengths packed; zslots: the same lengths in 2048-B slots at
         # +14 (a netmap RX ring of mixed sizes)
         n = args.packets if args.packets != (1 << 20) else (1 << 21 if args.config == "zslots"
@@ -146,7 +167,7 @@ def main():
     knobs = {"WC_SHAPE", "WC_NT", "WC_BLOCKS_PER_CU", "WC_GRID", "WC_FLAT_UN", "WC_FLAT_TPW",
              "WC_DIAG_NOLOAD", "WC_FLAT_MIN", "WC_RAGGED_SHAPE", "WC_VARIANT", "WC_SEG",
              "WC_SEG_ROWS", "WC_GRP_DENSE", "WC_GRP_SPARSE", "WC_GRP_ROWS",
-             "WC_STRIDED_SEG", "WC_FLAT_PK", "WC_GATHER"}
+             "WC_STRIDED_SEG", "WC_FLAT_PK", "WC_GATHER", "WC_RX_ROWS", "WC_RX_EARLY"}
     knobs |= {kv.split("=", 1)[0] for v in variants for kv in v.split()}
     knobs |= {k for k in os.environ if k.startswith("WC_") and k != "WC_NO_BUILD"}
     base_env = {k: os.environ.get(k) for k in knobs}
@@ -204,7 +225,7 @@ def main():
                     torch.cuda.synchronize()
                 ms = time_it(run, args.iters, stream)
                 if r == 0:
-                    res = out.cpu().numpy().view(np.uint16).copy()
+                    res = out.cpu().numpy().copy()
                     if ref is None:
                         ref = res
                     elif not np.array_equal(ref, res):

@@ -121,6 +121,9 @@ struct Config {
     int flat_pk = 1;               // WC_FLAT_PK: flat kernel chunks per lane slot
     int gather = 1;                // WC_GATHER: seg kernel's gathered-stream path (0 off, 2 forced)
     int lean_max = 48;             // WC_LEAN_MAX: lean kernel for aligned packets up to this many chunks
+    int rx_rows = 4;               // WC_RX_ROWS: RX verdict stream rows per group (2, 4)
+    int rx_early = 0;              // WC_RX_EARLY: RX verdict parses before streaming
+    int rx_mode() const { return (rx_rows == 2 ? wc::kRxRows2 : 0) | (rx_early ? wc::kRxEarly : 0); }
 };
 
 std::mutex g_mu;
@@ -196,6 +199,8 @@ void load_config_locked()
     c.flat_pk = env_int("WC_FLAT_PK", c.flat_pk);
     c.gather = env_int("WC_GATHER", c.gather);
     c.lean_max = env_int("WC_LEAN_MAX", c.lean_max);
+    c.rx_rows = env_int("WC_RX_ROWS", c.rx_rows);
+    c.rx_early = env_int("WC_RX_EARLY", c.rx_early);
     g_cfg = c;
     g_cfg_loaded = true;
 }
@@ -716,7 +721,7 @@ int run_ragged_any(const Device &D, const Config &C, const uint8_t *d_base, cons
 {
     if (kind == kKindRx)
         return hip_err(wc::launch_rx_verdict(d_base, d_off, d_len, n, (uint8_t *)d_out, nullptr,
-                                             C.nt != 0, st, C.variant));
+                                             C.nt != 0, st, C.rx_mode()));
     const Plan p = plan_ragged(D, C, n, kind, zero_copy);
     wc::LaunchArgs a{d_base, 0,       0,    d_off, d_len, n,
                      (uint16_t *)d_out, nullptr, kind, true,  false, C.nt != 0,
@@ -1265,7 +1270,7 @@ int wc_rx_verdict_ragged(const void *d_base, const uint64_t *d_off, const uint16
     if (rc)
         return rc;
     return hip_err(wc::launch_rx_verdict(d_base, d_off, d_frame_len, n, d_verdict, d_drops,
-                                         C.nt != 0, (hipStream_t)stream, C.variant));
+                                         C.nt != 0, (hipStream_t)stream, C.rx_mode()));
 }
 
 int wc_rx_verdict_host(const void *h_base, uint64_t h_bytes, const uint64_t *h_off,

@@ -165,8 +165,11 @@ hipError_t launch_synth(void *buf, uint64_t nbytes, uint64_t seed, int grid,
                         hipStream_t st);
 // RX verdicts of Ethernet frames [base + offs[i], + flens[i]) (wc_k_rx.hip);
 // drops (optional) accumulates the frames the reference's RX path drops.
+// mode: kRxRows2 (2-row stream groups instead of 4) | kRxEarly (parse, then
+// stream only the checked frames); every mode gives the same verdicts.
+constexpr int kRxRows2 = 1, kRxEarly = 2;
 hipError_t launch_rx_verdict(const void *base, const uint64_t *offs, const uint16_t *flens,
                              uint64_t n, uint8_t *verdict, uint64_t *drops, bool nt,
-                             hipStream_t st, int variant = 0);
+                             hipStream_t st, int mode = 0);
 
 } // namespace wc

@@ -231,8 +231,14 @@ __device__ __forceinline__ RxParse rx_parse_slow(uint64_t fa, uint32_t flen, boo
 
 
 // UNS: 64-chunk rows per row group of the gathered stream (4, as the seg
-// kernel's ragged default).
-template <int UNS, bool NT>
+// kernel's ragged default; 2 halves the rows in flight and the registers).
+// EARLY: the header parse completes BEFORE the stream, which then carries
+// only the frames that need the UDP check and only their checked range
+// [ip, ip + udp_len + hl) -- one load round trip per tile more, no bytes read
+// for frames the headers rule out (non-IP, non-UDP, bad IPv4 header,
+// fragments, zero UDP checksums); !EARLY streams every frame with >= 28 IP
+// bytes while the parse is in flight.
+template <int UNS, bool NT, bool EARLY>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
 k_rx_verdict(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
              const uint16_t *__restrict__ flens, uint64_t n, uint8_t *__restrict__ verdict,
@@ -266,44 +272,64 @@ k_rx_verdict(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
         const uint32_t flen = flen_n;
         meta_load(offs, flens, (tile + nwaves) * 64 + lane, n, off_n, flen_n);
 
-        // Header chunks first; then every frame that may need the UDP check
-        // (>= 28 IP bytes) streams its IP bytes [ip, ip + room) as the seg
-        // path's gathered stream, and the parse completes once that stream's
-        // first row group is in flight (seg_tile's Late hook): the checked
-        // range [ip, ip + udp_len + hl) is a prefix of the streamed one.
-        // Frames that turn out not to need the check were read for nothing.
         u32x4 c[5];
         rx_load(fa, flen, valid, zero, c);
         const uint64_t ip = fa + 14u;
-        const uint32_t room = flen >= 14u ? flen - 14u : 0u;
-        const bool spec = valid && room >= 28u;
         bool slow = false;
         RxParse h{};
         uint32_t v;
-        if (__ballot(spec)) {
-            const FlatTile t = flat_tile_setup<UNS, 1>(L.f, lane, ip, room, room, spec, 0u);
-            bool need = false;
-            auto late = [&](uint32_t &len, bool &on) {
-                h = rx_parse(c, fa, flen, valid, slow);
-                need = h.need && !slow;
-                on = need;
-                len = need ? h.plen : 0u;
-            };
-            bool done = true;
-            uint16_t rh = 0;
-            uint16_t r = seg_tile<UNS, WC_KIND_PAYLOAD, NT, false, GathSrc<UNS, NT>, true,
-                                  decltype(late)>(
-                L.f.pre, L.stage, L.pm, lane, ip, 16ull * t.cp + (ip & 15u), room, spec,
-                t.total, GathSrc<UNS, NT>{&L.f, t}, zero, done, rh, late);
-            if (need && !done) // header longer than the packet, or a possible wrap
-                r = lane_payload_exact<NT>(ip, h.plen);
-            v = h.verdict;
-            if (need)
-                v = r != 0 ? kRxBadUdpCksum : kRxOk; // udp.c:134-139
-            wave_order(); // the tables are rewritten by the next tile
-        } else {
+        if constexpr (EARLY) {
             h = rx_parse(c, fa, flen, valid, slow);
             v = h.verdict;
+            const bool need = h.need && !slow;
+            if (__ballot(need)) {
+                const FlatTile t = flat_tile_setup<UNS, 1>(L.f, lane, ip, h.plen, h.plen, need, 0u);
+                bool done = true;
+                uint16_t rh = 0;
+                uint16_t r = seg_tile<UNS, WC_KIND_PAYLOAD, NT, false, GathSrc<UNS, NT>, true>(
+                    L.f.pre, L.stage, L.pm, lane, ip, 16ull * t.cp + (ip & 15u), h.plen, need,
+                    t.total, GathSrc<UNS, NT>{&L.f, t}, zero, done, rh);
+                if (need && !done) // header longer than the packet, or a possible wrap
+                    r = lane_payload_exact<NT>(ip, h.plen);
+                if (need)
+                    v = r != 0 ? kRxBadUdpCksum : kRxOk; // udp.c:134-139
+                wave_order(); // the tables are rewritten by the next tile
+            }
+        } else {
+            // Header chunks first; then every frame that may need the UDP
+            // check (>= 28 IP bytes) streams its IP bytes [ip, ip + room) as
+            // the seg path's gathered stream, and the parse completes once
+            // that stream's first row group is in flight (seg_tile's Late
+            // hook): the checked range [ip, ip + udp_len + hl) is a prefix of
+            // the streamed one.  Frames that turn out not to need the check
+            // were read for nothing.
+            const uint32_t room = flen >= 14u ? flen - 14u : 0u;
+            const bool spec = valid && room >= 28u;
+            if (__ballot(spec)) {
+                const FlatTile t = flat_tile_setup<UNS, 1>(L.f, lane, ip, room, room, spec, 0u);
+                bool need = false;
+                auto late = [&](uint32_t &len, bool &on) {
+                    h = rx_parse(c, fa, flen, valid, slow);
+                    need = h.need && !slow;
+                    on = need;
+                    len = need ? h.plen : 0u;
+                };
+                bool done = true;
+                uint16_t rh = 0;
+                uint16_t r = seg_tile<UNS, WC_KIND_PAYLOAD, NT, false, GathSrc<UNS, NT>, true,
+                                      decltype(late)>(
+                    L.f.pre, L.stage, L.pm, lane, ip, 16ull * t.cp + (ip & 15u), room, spec,
+                    t.total, GathSrc<UNS, NT>{&L.f, t}, zero, done, rh, late);
+                if (need && !done) // header longer than the packet, or a possible wrap
+                    r = lane_payload_exact<NT>(ip, h.plen);
+                v = h.verdict;
+                if (need)
+                    v = r != 0 ? kRxBadUdpCksum : kRxOk; // udp.c:134-139
+                wave_order(); // the tables are rewritten by the next tile
+            } else {
+                h = rx_parse(c, fa, flen, valid, slow);
+                v = h.verdict;
+            }
         }
         if (__ballot(slow)) { // IPv4 headers with more than 20 B of options, IHL < 5
             const RxParse hs = rx_parse_slow(fa, flen, slow, zero);
@@ -328,20 +354,28 @@ k_rx_verdict(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
 
 hipError_t launch_rx_verdict(const void *base, const uint64_t *offs, const uint16_t *flens,
                              uint64_t n, uint8_t *verdict, uint64_t *drops, bool nt,
-                             hipStream_t st, int variant)
+                             hipStream_t st, int mode)
 {
-    (void)variant; // (tuning build: A/B branches)
     const uint64_t tiles = (n + 63) / 64;
     const int grid = (int)std::min<uint64_t>(
         kMaxGridBlocks, std::max<uint64_t>(1, (tiles + kFlatWaves - 1) / kFlatWaves));
-    if (nt)
-        hipLaunchKernelGGL((k_rx_verdict<4, true>), dim3(grid), dim3(256), 0, st,
-                           (const uint8_t *)base, offs, flens, n, verdict,
-                           (unsigned long long *)drops);
-    else
-        hipLaunchKernelGGL((k_rx_verdict<4, false>), dim3(grid), dim3(256), 0, st,
-                           (const uint8_t *)base, offs, flens, n, verdict,
-                           (unsigned long long *)drops);
+    const bool rows2 = (mode & kRxRows2) != 0, early = (mode & kRxEarly) != 0;
+#define WC_RX_LAUNCH(U, N, E)                                                  \
+    hipLaunchKernelGGL((k_rx_verdict<U, N, E>), dim3(grid), dim3(256), 0, st,  \
+                       (const uint8_t *)base, offs, flens, n, verdict,         \
+                       (unsigned long long *)drops)
+    const int sel = (nt ? 4 : 0) | (rows2 ? 2 : 0) | (early ? 1 : 0);
+    switch (sel) {
+    case 7: WC_RX_LAUNCH(2, true, true); break;
+    case 6: WC_RX_LAUNCH(2, true, false); break;
+    case 5: WC_RX_LAUNCH(4, true, true); break;
+    case 4: WC_RX_LAUNCH(4, true, false); break;
+    case 3: WC_RX_LAUNCH(2, false, true); break;
+    case 2: WC_RX_LAUNCH(2, false, false); break;
+    case 1: WC_RX_LAUNCH(4, false, true); break;
+    default: WC_RX_LAUNCH(4, false, false); break;
+    }
+#undef WC_RX_LAUNCH
     return hipGetLastError();
 }
 
