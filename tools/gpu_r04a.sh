@@ -12,3 +12,8 @@ for a in "--config zrx" "--config rx" "--config zrx --rx-arp 3"; do
   timeout -k 10 200 python tools/tune.py $a --rounds 5 --iters 20 --variants "$V" >> gpurun_out/r04a/tune_rx.log 2>&1 || exit 1
 done
 cat gpurun_out/r04a/tune_rx.log | grep -v amdgpu
+echo "== C4 store A/B (tuning build: bit 24 drops the result store)" >> gpurun_out/r04a/tune_store.log
+timeout -k 10 200 python tools/tune.py --config c4 --rounds 5 --iters 10 --variants "default;WC_VARIANT=16777216" >> gpurun_out/r04a/tune_store.log 2>&1 || exit 1
+grep -v amdgpu gpurun_out/r04a/tune_store.log
+(cd /tmp && timeout -k 10 60 rocprofv3 -L) > gpurun_out/r04a/counters.txt 2>&1 || true
+grep -c . gpurun_out/r04a/counters.txt

@@ -181,10 +181,14 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
         // results' HBM writes themselves cost C4 ~30 us per 32 MB array
         // whatever their form -- 16-byte chunks, one 512-B run per block of
         // tiles, nt / sc1 (profiles/ab_r03_fused_store.log).
+        // (Tuning build only, for the write-cost counters of DESIGN.md
+        // section 10: WC_VARIANT bit 24 drops the result store, bit 25 the
+        // header-checksum store -- results are then missing.)
         if (valid) {
             if constexpr (HDR)
-                out_hdr[p] = rh;
-            if (out)
+                if (!(variant & (1 << 25)))
+                    out_hdr[p] = rh;
+            if (out && !(variant & (1 << 24)))
                 out[p] = r;
         }
         nbad += valid && r != 0;
