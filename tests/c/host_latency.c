@@ -9,10 +9,13 @@
  * backend's pool, backend_sock.c:145), slots picked at random; well-formed
  * Ethernet + IPv4 + UDP frames with valid checksums for the RX verdict.  For
  * n packets and L bytes, one JSON line with the median (and p90) per call of:
- *   zc_us        wc_cksum_host, pool registered (zero-copy: one kernel reads
- *                the packets in place)
+ *   srv_us       wc_cksum_host, pool registered, batch answered by the
+ *                resident server (no launch, no sync: WC_SERVE=1, n <= 256)
+ *   zc_us        wc_cksum_host, pool registered, one zero-copy kernel launch
+ *                per call reading the packets in place (WC_SERVE=0)
  *   pipe_us      wc_cksum_host, pool not registered (pinned staging + copies)
- *   rx_zc_us     wc_rx_verdict_host, pool registered
+ *   rx_srv_us / rx_zc_us   wc_rx_verdict_host, pool registered, server /
+ *                launch
  *   floor_us     wc_cksum_strided on 1 device-resident packet + stream sync:
  *                the launch + completion floor, no PCIe data
  *   cpu1_us / cpuN_us      oracle_cksum_ragged, 1 / N threads
@@ -213,7 +216,28 @@ int main(int argc, char **argv)
             c.verdict = verdict;
             c.n = n;
             double zc, zc9, pp, pp9, rx, rx9, fl, fl9, c1, c19, cn, cn9, r1, r19;
+            double sv = -1, sv9 = -1, rs = -1, rs9 = -1;
             c.pool = pool;
+            if (n <= 256) {
+                setenv("WC_SERVE", "1", 1);
+                wc_config_reload();
+                memset(out, 0, n * 2);
+                time_calls(c_host, &c, secs, &sv, &sv9);
+                oracle_cksum_ragged(pool, off, len, n, want, ORACLE_KIND_IP, 1);
+                if (memcmp(out, want, n * 2)) {
+                    printf("host_latency: FAIL server n=%llu L=%u\n", (unsigned long long)n, L);
+                    return 1;
+                }
+                memset(verdict, 0xEE, n);
+                time_calls(c_rx, &c, secs, &rs, &rs9);
+                oracle_rx_verdict_ragged(pool, off, flen, n, vwant, 1);
+                if (memcmp(verdict, vwant, n)) {
+                    printf("host_latency: FAIL server rx n=%llu L=%u\n", (unsigned long long)n, L);
+                    return 1;
+                }
+            }
+            setenv("WC_SERVE", "0", 1);
+            wc_config_reload();
             time_calls(c_host, &c, secs, &zc, &zc9);
             oracle_cksum_ragged(pool, off, len, n, want, ORACLE_KIND_IP, 1);
             if (memcmp(out, want, n * 2)) {
@@ -246,11 +270,14 @@ int main(int argc, char **argv)
             c.threads = threads;
             time_calls(c_cpu, &c, secs / 2, &cn, &cn9);
             time_calls(c_cpu_rx, &c, secs / 2, &r1, &r19);
-            printf("{\"n\": %llu, \"L\": %u, \"zc_us\": %.2f, \"zc_p90_us\": %.2f, "
-                   "\"pipe_us\": %.2f, \"rx_zc_us\": %.2f, \"rx_zc_p90_us\": %.2f, "
+            printf("{\"n\": %llu, \"L\": %u, \"srv_us\": %.2f, \"srv_p90_us\": %.2f, "
+                   "\"zc_us\": %.2f, \"zc_p90_us\": %.2f, "
+                   "\"pipe_us\": %.2f, \"rx_srv_us\": %.2f, \"rx_srv_p90_us\": %.2f, "
+                   "\"rx_zc_us\": %.2f, \"rx_zc_p90_us\": %.2f, "
                    "\"floor_us\": %.2f, \"cpu1_us\": %.3f, \"cpu%d_us\": %.2f, "
                    "\"cpu1_rx_us\": %.3f}\n",
-                   (unsigned long long)n, L, zc, zc9, pp, rx, rx9, fl, c1, threads, cn, r1);
+                   (unsigned long long)n, L, sv, sv9, zc, zc9, pp, rs, rs9, rx, rx9, fl, c1,
+                   threads, cn, r1);
             fflush(stdout);
         }
     }

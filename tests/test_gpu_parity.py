@@ -764,6 +764,53 @@ def test_host_zero_copy_small_batches(gpu, kind, n):
     np.testing.assert_array_equal(got, want)
 
 
+@pytest.mark.parametrize("waves", ["64", "7"])
+def test_host_resident_server(gpu, monkeypatch, waves):
+    """Small registered batches answered by the resident server (wc_k_serve:
+    no launch per call) are exact for both kinds over every start phase and
+    length up to the server's 4064-B limit (and past it: the launch path),
+    batches larger than the wave count (several packets per wave) included;
+    the server stops when idle and restarts on the next call."""
+    import time
+    monkeypatch.setenv("WC_SERVE_WAVES", waves)
+    monkeypatch.setenv("WC_SERVE_MAX", "1024")
+    wc.reload_config()
+    rng = np.random.default_rng(int(waves))
+    slot = 8192
+    pool = rng.integers(0, 256, 512 * slot, dtype=np.uint8)
+    wc.host_register(pool)
+    try:
+        for n in (1, 2, 7, 64, 65, 300, 1024):
+            for kind in ("ip", "payload"):
+                slots = rng.permutation(512)[: min(n, 512)]
+                slots = np.resize(slots, n)  # n > 512: slots reused (overlap is fine)
+                offs = (slots.astype(np.uint64) * slot + rng.integers(0, 16, n).astype(np.uint64))
+                lens = rng.integers(0, 4065, n).astype(np.uint16)
+                lens[: min(n, 4)] = [0, 1, 4064, 4063][: min(n, 4)]
+                if n == 7:
+                    lens[6] = 4065  # past the server's limit: the launch path
+                if kind == "payload":
+                    pkts = random_packets(rng, n, max_payload=3000, wild=True)
+                    for o, (p, ln) in zip(offs, pkts):
+                        pool[int(o): int(o) + len(p)] = np.frombuffer(p, dtype=np.uint8)
+                    lens = np.array([ln for _, ln in pkts], dtype=np.uint16)
+                k = 0 if kind == "ip" else 1
+                want = c_oracle.cksum_ragged(pool, offs, lens, kind=k)
+                got = wc.cksum_host(pool, offs, lens, kind=kind)
+                np.testing.assert_array_equal(got, want, err_msg=f"n={n} {kind}")
+        time.sleep(0.1)  # idle: the watcher stops the grid
+        torch.cuda.synchronize()
+        offs = np.arange(64, dtype=np.uint64) * slot + 5
+        lens = np.full(64, 1472, dtype=np.uint16)
+        np.testing.assert_array_equal(wc.cksum_host(pool, offs, lens),
+                                      c_oracle.cksum_ragged(pool, offs, lens))
+    finally:
+        wc.host_unregister(pool)
+        monkeypatch.delenv("WC_SERVE_WAVES")
+        monkeypatch.delenv("WC_SERVE_MAX")
+        wc.reload_config()
+
+
 def test_host_register_after_free_and_reuse(gpu):
     """register -> free without unregister -> a new buffer mapped at the same
     address -> register again: the zero-copy path must read the NEW pages

@@ -35,7 +35,8 @@ ORACLE_DIR = ROOT / "oracle"
 
 HIP_SOURCES = [CSRC / "wc_k_strided.hip", CSRC / "wc_k_lean.hip", CSRC / "wc_k_seg.hip",
                CSRC / "wc_k_flat.hip",
-               CSRC / "wc_k_rx.hip", CSRC / "wc_rccl.cpp", CSRC / "wc_k_synth.hip",
+               CSRC / "wc_k_rx.hip", CSRC / "wc_k_serve.hip", CSRC / "wc_rccl.cpp",
+               CSRC / "wc_k_synth.hip",
                CSRC / "wc_cksum_api.cpp"]
 HIP_DEPS = HIP_SOURCES + [CSRC / "wc_cksum_kernels.h", CSRC / "wc_rccl.h", CSRC / "wc_device.h",
                           CSRC / "wc_flat.h", CSRC / "wc_seg.h",

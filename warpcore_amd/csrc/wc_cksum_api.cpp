@@ -16,6 +16,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -72,9 +74,23 @@ struct ZeroCopy {
     bool ready = false;
 };
 
+// The resident small-batch server of one device (wc_k_serve.hip): its
+// stream, the mapped pinned request records and result slots, the request
+// counter, and whether its grid is running.
+struct Server {
+    hipStream_t st = nullptr;
+    wc::SrvRec *h_rec = nullptr, *d_rec = nullptr;
+    wc::SrvRes *h_res = nullptr, *d_res = nullptr;
+    uint32_t seq = 0;
+    int waves = 0;
+    bool ready = false, running = false, broken = false;
+    std::chrono::steady_clock::time_point last{};
+};
+
 struct Device {
     bool ok = false;
     int cus = 0;
+    uint64_t clock_khz = 100000; // wall_clock64 rate (hipDeviceAttributeWallClockRate)
     hipStream_t scalar_st = nullptr;
     uint8_t *h_stage = nullptr;  // pinned + mapped scalar staging
     uint8_t *d_stage = nullptr;
@@ -82,6 +98,7 @@ struct Device {
     uint16_t *d_res = nullptr;
     HostPipe pipe;
     ZeroCopy zc;
+    Server srv;
 };
 
 struct Registration {
@@ -121,6 +138,10 @@ struct Config {
     int flat_pk = 1;               // WC_FLAT_PK: flat kernel chunks per lane slot
     int gather = 1;                // WC_GATHER: seg kernel's gathered-stream path (0 off, 2 forced)
     int lean_max = 48;             // WC_LEAN_MAX: lean kernel for aligned packets up to this many chunks
+    int serve = 1;                 // WC_SERVE: resident server for small registered host batches
+    int serve_waves = 64;          // WC_SERVE_WAVES: its waves (one 64-lane workgroup each)
+    int serve_max = 256;           // WC_SERVE_MAX: largest batch (packets) it takes
+    int serve_idle_us = 20000;     // WC_SERVE_IDLE_US: stopped after this long without a call
     int rx_rows = 4;               // WC_RX_ROWS: RX verdict stream rows per group (2, 4)
     int rx_early = 0;              // WC_RX_EARLY: RX verdict parses before streaming
     int rx_mode() const { return (rx_rows == 2 ? wc::kRxRows2 : 0) | (rx_early ? wc::kRxEarly : 0); }
@@ -199,6 +220,10 @@ void load_config_locked()
     c.flat_pk = env_int("WC_FLAT_PK", c.flat_pk);
     c.gather = env_int("WC_GATHER", c.gather);
     c.lean_max = env_int("WC_LEAN_MAX", c.lean_max);
+    c.serve = env_int("WC_SERVE", c.serve);
+    c.serve_waves = std::max(1, std::min(env_int("WC_SERVE_WAVES", c.serve_waves), 1024));
+    c.serve_max = std::max(0, std::min(env_int("WC_SERVE_MAX", c.serve_max), (int)wc::kSrvMaxPkts));
+    c.serve_idle_us = std::max(100, env_int("WC_SERVE_IDLE_US", c.serve_idle_us));
     c.rx_rows = env_int("WC_RX_ROWS", c.rx_rows);
     c.rx_early = env_int("WC_RX_EARLY", c.rx_early);
     g_cfg = c;
@@ -248,6 +273,10 @@ int init_locked(int device, Device **out)
             return WC_ENODEV;
         }
         D.cus = prop.multiProcessorCount;
+        int khz = 0;
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess &&
+            khz > 0)
+            D.clock_khz = (uint64_t)khz;
         e = hipStreamCreateWithFlags(&D.scalar_st, hipStreamNonBlocking);
         if (e != hipSuccess)
             return hip_err(e);
@@ -729,6 +758,184 @@ int run_ragged_any(const Device &D, const Config &C, const uint8_t *d_base, cons
     return run(D, C, a, p, st);
 }
 
+// ---------------------------------------------------------------------------
+// The resident small-batch server (wc_k_serve.hip).  A small batch in a
+// registered region is answered by a persistent grid that polls request
+// records in mapped pinned memory: no launch, no stream synchronisation, no
+// copy per call.  The grid is started by the first such call, kept while
+// calls keep coming, and stopped (stop flag in every record, then the stream
+// drained) by the idle watcher after WC_SERVE_IDLE_US without a call, by
+// wc_gpu_fini, or at process exit -- so it never outlives its process.  If it
+// ever fails to answer, the call falls back to the zero-copy launch and the
+// server stays off for the process.
+
+constexpr int kSrvFallback = 1; // serve_batch: not served, take the launch path
+constexpr uint64_t kSrvSafetyMs = 4000; // the grid drains itself after this idle time
+
+std::atomic<bool> g_srv_quit{false};
+std::thread g_srv_watcher;
+bool g_srv_hooks = false; // watcher started, atexit registered
+
+int server_init_locked(Server &S)
+{
+    if (S.ready)
+        return WC_OK;
+    const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
+    if (hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking) != hipSuccess ||
+        hipHostMalloc((void **)&S.h_rec, wc::kSrvMaxPkts * sizeof(wc::SrvRec), fl) != hipSuccess ||
+        hipHostMalloc((void **)&S.h_res, wc::kSrvMaxPkts * sizeof(wc::SrvRes), fl) != hipSuccess ||
+        hipHostGetDevicePointer((void **)&S.d_rec, S.h_rec, 0) != hipSuccess ||
+        hipHostGetDevicePointer((void **)&S.d_res, S.h_res, 0) != hipSuccess)
+        return WC_ENOMEM;
+    memset(S.h_rec, 0, wc::kSrvMaxPkts * sizeof(wc::SrvRec));
+    memset((void *)S.h_res, 0, wc::kSrvMaxPkts * sizeof(wc::SrvRes));
+    S.ready = true;
+    return WC_OK;
+}
+
+// Launch the grid over the records as they stand (the kernel serves any
+// record whose seq differs from seq0).  With `reset`, every record is first
+// rewritten to {seq, no stop}: nothing pending, stop flags cleared.
+int server_launch_locked(Device &D, int dev, bool reset, uint32_t seq0)
+{
+    Server &S = D.srv;
+    if (reset)
+        for (uint32_t k = 0; k < wc::kSrvMaxPkts; ++k) {
+            S.h_rec[k].addr = 0;
+            S.h_rec[k].info = 0;
+            __atomic_store_n(&S.h_rec[k].seq, seq0, __ATOMIC_RELEASE);
+        }
+    (void)dev;
+    const uint64_t idle_ticks = kSrvSafetyMs * D.clock_khz;
+    const hipError_t e = wc::launch_serve(S.d_rec, S.d_res, seq0, S.waves, idle_ticks, S.st);
+    if (e != hipSuccess)
+        return hip_err(e);
+    S.running = true;
+    return WC_OK;
+}
+
+// Stop flag in every polled record, then wait for the grid to drain.
+void server_stop_locked(Device &D, int dev)
+{
+    Server &S = D.srv;
+    if (!S.running)
+        return;
+    for (int k = 0; k < S.waves && k < (int)wc::kSrvMaxPkts; ++k)
+        __atomic_store_n(&S.h_rec[k].info, 1u << 24, __ATOMIC_RELEASE);
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(dev);
+    (void)hipStreamSynchronize(S.st);
+    if (cur >= 0)
+        (void)hipSetDevice(cur);
+    S.running = false;
+}
+
+void server_stop_all_locked()
+{
+    for (int d = 0; d < kMaxDevices; ++d)
+        if (g_dev[d].ok && g_dev[d].srv.running)
+            server_stop_locked(g_dev[d], d);
+}
+
+void server_watch()
+{
+    while (!g_srv_quit.load()) {
+        std::this_thread::sleep_for(std::chrono::milliseconds(2));
+        std::lock_guard<std::mutex> lk(g_mu);
+        const auto now = std::chrono::steady_clock::now();
+        for (int d = 0; d < kMaxDevices; ++d) {
+            Device &D = g_dev[d];
+            if (D.ok && D.srv.running &&
+                now - D.srv.last > std::chrono::microseconds(g_cfg.serve_idle_us))
+                server_stop_locked(D, d);
+        }
+    }
+}
+
+void server_atexit()
+{
+    g_srv_quit.store(true);
+    if (g_srv_watcher.joinable())
+        g_srv_watcher.join();
+    std::lock_guard<std::mutex> lk(g_mu);
+    server_stop_all_locked();
+}
+
+// One small registered batch through the server (caller holds g_mu, the
+// device is current).  Returns kSrvFallback when the server can't take it.
+int serve_batch(Device &D, int dev, const uint8_t *dbase, const uint64_t *h_off,
+                const uint16_t *h_len, uint64_t n, uint8_t *h_out, int kind)
+{
+    Server &S = D.srv;
+    if (S.broken)
+        return kSrvFallback;
+    int rc = server_init_locked(S);
+    if (rc)
+        return rc;
+    if (!g_srv_hooks) {
+        g_srv_hooks = true;
+        g_srv_watcher = std::thread(server_watch);
+        std::atexit(server_atexit);
+    }
+    if (!S.running) {
+        S.waves = g_cfg.serve_waves;
+        rc = server_launch_locked(D, dev, true, S.seq);
+        if (rc)
+            return rc;
+    }
+    uint32_t seq = S.seq + 1;
+    if (seq == 0) // 0 is the records' initial value
+        seq = 1;
+    S.seq = seq;
+    const uint32_t rkind = kind == kKindRx ? wc::kSrvKindRx : (uint32_t)kind;
+    // Last packet first: a wave that sees its first record current finds
+    // every later one of the request current too (stores become visible in
+    // program order).
+    for (uint64_t k = n; k-- > 0;) {
+        wc::SrvRec &r = S.h_rec[k];
+        r.addr = (uint64_t)(dbase + h_off[k]);
+        r.info = (uint32_t)h_len[k] | (rkind << 16);
+        __atomic_store_n(&r.seq, seq, __ATOMIC_RELEASE);
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    bool relaunched = false;
+    for (uint64_t k = 0; k < n; ++k) {
+        for (uint32_t spin = 1;; ++spin) {
+            if (__atomic_load_n(&S.h_res[k].seq, __ATOMIC_ACQUIRE) == seq)
+                break;
+            __builtin_ia32_pause();
+            if (spin % 4096)
+                continue;
+            const auto dt = std::chrono::steady_clock::now() - t0;
+            if (dt > std::chrono::milliseconds(50) && !relaunched &&
+                hipStreamQuery(S.st) == hipSuccess) {
+                // the grid had drained (its own idle limit): serve again
+                relaunched = true;
+                rc = server_launch_locked(D, dev, false, seq - 1);
+                if (rc)
+                    return rc;
+            }
+            if (dt > std::chrono::milliseconds(2000)) {
+                fprintf(stderr, "wccksum: resident server did not answer; using launches\n");
+                server_stop_locked(D, dev);
+                S.broken = true;
+                return kSrvFallback;
+            }
+        }
+    }
+    if (kind == kKindRx) {
+        for (uint64_t k = 0; k < n; ++k)
+            h_out[k] = (uint8_t)S.h_res[k].value;
+    } else {
+        uint16_t *o = (uint16_t *)h_out;
+        for (uint64_t k = 0; k < n; ++k)
+            o[k] = (uint16_t)S.h_res[k].value;
+    }
+    S.last = std::chrono::steady_clock::now();
+    return WC_OK;
+}
+
 // Small registered batch: one launch reading host memory in place.
 int host_zero_copy(Device &D, const uint8_t *dbase, const uint64_t *h_off,
                    const uint16_t *h_len, uint64_t n, uint8_t *h_out, int kind)
@@ -1107,6 +1314,17 @@ int host_batch(const void *h_base, uint64_t h_bytes, const uint64_t *h_off,
     if (rc)
         return rc;
     const uint8_t *dbase = registered_dptr_locked(h_base, h_bytes);
+    if (dbase && g_cfg.serve && n <= (uint64_t)g_cfg.serve_max) {
+        bool fits = true;
+        for (uint64_t i = 0; i < n && fits; ++i)
+            fits = span_of(h_len[i], kind) <= wc::kSrvMaxBytes;
+        int dev = 0;
+        if (fits && current_device(&dev) == WC_OK) {
+            rc = serve_batch(*D, dev, dbase, h_off, h_len, n, h_out, kind);
+            if (rc != kSrvFallback)
+                return rc;
+        }
+    }
     if (dbase && n <= kZcPkts && total <= (uint64_t)g_cfg.zc_bytes)
         return host_zero_copy(*D, dbase, h_off, h_len, n, h_out, kind);
     rc = pipe_init_locked(D->pipe);
@@ -1505,6 +1723,7 @@ int wc_gpu_fini(void)
     std::lock_guard<std::mutex> lk(g_mu);
     int cur = 0;
     const bool have_cur = hipGetDevice(&cur) == hipSuccess;
+    server_stop_all_locked();
     wc::rccl_fini();
     for (int g = 0; g < g_multi_n; ++g) {
         (void)hipSetDevice(g_shard[g].dev);
@@ -1524,6 +1743,11 @@ int wc_gpu_fini(void)
             (void)hipHostFree(D.zc.h_off);
             (void)hipHostFree(D.zc.h_len);
             (void)hipHostFree(D.zc.h_out);
+        }
+        if (D.srv.ready) {
+            (void)hipStreamDestroy(D.srv.st);
+            (void)hipHostFree(D.srv.h_rec);
+            (void)hipHostFree(D.srv.h_res);
         }
         (void)hipStreamSynchronize(D.scalar_st);
         (void)hipStreamDestroy(D.scalar_st);

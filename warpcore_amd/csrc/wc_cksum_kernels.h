@@ -172,4 +172,23 @@ hipError_t launch_rx_verdict(const void *base, const uint64_t *offs, const uint1
                              uint64_t n, uint8_t *verdict, uint64_t *drops, bool nt,
                              hipStream_t st, int mode = 0);
 
+// Resident small-batch server (wc_k_serve.hip).  Host-mapped pinned memory:
+// one record per packet, written by the host (seq last), polled / read by the
+// server's waves; one result slot per packet, written by the GPU in one
+// 8-byte store.  Requests are numbered by seq (never 0 after the first).
+constexpr uint32_t kSrvMaxPkts = 1024;  // packets per request
+constexpr uint32_t kSrvMaxBytes = 4064; // bytes one packet (frame) may span
+constexpr uint32_t kSrvKindRx = 2;      // record kind beside WC_KIND_IP / _PAYLOAD
+struct alignas(16) SrvRec {
+    uint64_t addr; // device address of the packet / frame
+    uint32_t info; // len | kind << 16 | stop << 24
+    uint32_t seq;  // request number, stored last
+};
+struct alignas(8) SrvRes {
+    uint32_t value; // checksum or RX verdict
+    uint32_t seq;   // the request it answers
+};
+hipError_t launch_serve(const SrvRec *d_recs, SrvRes *d_res, uint32_t seq0, int waves,
+                        uint64_t idle_ticks, hipStream_t st);
+
 } // namespace wc
