@@ -92,6 +92,10 @@ def parse(argv=None):
     ap.add_argument("--total-packets", type=int, default=1 << 28, help="c5 total")
     ap.add_argument("--window-packets", type=int, default=1 << 25, help="c5 resident window")
     ap.add_argument("--packets", type=int, default=1 << 20)
+    ap.add_argument("--stride", type=int, default=0,
+                    help="c2/c3: packet stride (default: the packet length, packed)")
+    ap.add_argument("--offset", type=int, default=0,
+                    help="c2/c3: byte offset of packet 0 (14: IP packets in netmap slots)")
     ap.add_argument("--batches", type=int, default=0,
                     help="c2/c3: distinct batches the steps rotate over (0: enough for "
                          "--rotate-bytes)")
@@ -226,7 +230,7 @@ def make_workload(args, dev, rank, world):
                 "kind": kind}
         return SimpleNamespace(step=step, n=share, nbytes=share * L,
                                batches=[{"buf": buf, "out": out}], plan=plan, desc=desc,
-                               meta=meta, shape=(L, L), scaling="strong")
+                               meta=meta, shape=(L, L, 0), scaling="strong")
     if args.config in ("rx", "zrx"):
         # netmap RX ring (backend_netmap.c:379-391): one well-formed UDP
         # frame per 2048-B slot, valid IPv4 header and UDP checksums; one
@@ -266,14 +270,18 @@ def make_workload(args, dev, rank, world):
     if args.config in ("c2", "c3"):
         L = 1472 if args.config == "c2" else args.len
         n = args.packets
+        stride, at = args.stride or L, args.offset
         nbytes = n * L
-        K = rotation(nbytes, args)
+        span = at + n * stride
+        # bytes the steps touch: whole packets, or (sparse slots) a packet's
+        # lines -- the footprint the rotation must carry past the L3
+        K = rotation(n * min(stride, L + 128) if stride > L else nbytes, args)
         batches = []
         for k in range(K):
-            buf = torch.empty(nbytes + 64, dtype=torch.uint8, device=dev)
-            wc.synth_fill(buf, seed + k * BATCH_SEED_STEP, nbytes=nbytes)
+            buf = torch.empty(span + 64, dtype=torch.uint8, device=dev)
+            wc.synth_fill(buf, seed + k * BATCH_SEED_STEP, nbytes=span)
             if args.headers:
-                synth.stamp_udp_headers(buf, torch.arange(n, device=dev) * L,
+                synth.stamp_udp_headers(buf, torch.arange(n, device=dev) * stride + at,
                                         torch.full((n,), L, device=dev))
             batches.append({"buf": buf, "out": torch.empty(n, dtype=torch.uint16, device=dev),
                             "out_hdr": torch.empty(n, dtype=torch.uint16, device=dev)
@@ -282,22 +290,27 @@ def make_workload(args, dev, rank, world):
         def step(i=0):
             b = batches[i % K]
             if fused:
-                wc.cksum_ip_udp_strided(b["buf"], L, L, n, out_hdr=b["out_hdr"], out=b["out"])
+                wc.cksum_ip_udp_strided(b["buf"], stride, L, n, out_hdr=b["out_hdr"],
+                                        out=b["out"], byte_offset=at)
             else:
-                wc.cksum_strided(b["buf"], L, L, n, out=b["out"], kind=kind)
+                wc.cksum_strided(b["buf"], stride, L, n, out=b["out"], kind=kind, byte_offset=at)
 
-        plan = wc.plan_strided(batches[0]["buf"].data_ptr(), L, L, n, kind=kind)
+        plan = wc.plan_strided(batches[0]["buf"].data_ptr() + at, stride, L, n, kind=kind)
         desc = (f"C2: {n} x {L} B packets, stride {L}, device-resident"
-                if args.config == "c2" else f"C3: {n} x {L} B packets, stride {L}")
+                if args.config == "c2" else f"C3: {n} x {L} B packets, stride {stride}")
+        if at:
+            desc += f", packet 0 at +{at}"
         if K > 1:
-            desc += (f"; steps rotate over {K} distinct batches ({K * nbytes / GIB:.2f} GiB, "
+            desc += (f"; steps rotate over {K} distinct batches ({K * span / GIB:.2f} GiB, "
                      f"past the 256 MiB Infinity Cache)")
         meta = {"packets_per_gpu": n, "packet_bytes": L, "layout": "strided", "kind": kind,
-                "batches": K, "footprint_bytes": K * nbytes}
+                "batches": K, "footprint_bytes": K * span}
+        if stride != L or at:
+            meta.update(stride=stride, offset=at)
         if fused:
             desc += ", fused IPv4 header + payload_cksum pass"
         return SimpleNamespace(step=step, n=n, nbytes=nbytes, batches=batches, plan=plan,
-                               desc=desc, meta=meta, shape=(L, L), scaling="weak")
+                               desc=desc, meta=meta, shape=(L, stride, at), scaling="weak")
     if args.config in ("slots", "zslots"):
         # netmap RX ring drained into one ragged batch: one IP packet per
         # 2048-B slot at +14 (eth.h:44-48); slots = fixed --len + 28 B,
@@ -482,10 +495,10 @@ def cpu_baseline(args, buf, shape, nbytes_total):
     trials = 5
     per_trial = max(args.cpu_seconds / (2 * trials), 0.05)
     if args.config in ("c2", "c3", "c5"):
-        L, stride = shape
+        L, stride, at = shape
         # The whole batch (DRAM-resident on the host, far beyond its L3).
-        n_s = max(1, min(args.packets, (2 << 30) // L))
-        sample = buf[: n_s * stride].cpu().numpy()
+        n_s = max(1, min(args.packets, (2 << 30) // max(L, 1)))
+        sample = buf[at: at + n_s * stride].cpu().numpy()
 
         def trial(th):
             bps, passes = c_oracle.bench_strided(sample, stride, L, n_s, kind=k, threads=th,
@@ -558,18 +571,18 @@ def parity_batch(args, b, shape):
             "verdicts_ok": int(np.isin(want, (0, 1)).sum())}
     got = out.cpu().numpy().view(np.uint16)
     if args.config in ("c2", "c3", "c5"):
-        hb = buf[: got.size * shape[1]].cpu().numpy()
+        hb = buf[: shape[2] + got.size * shape[1]].cpu().numpy()
     else:  # ragged: every byte up to the last packet's end (+ its header fields)
         offs, lens = shape
         hb = buf[: min(buf.numel(), int(offs[-1]) + max(int(lens[-1]), 40))].cpu().numpy()
     if args.config in ("c2", "c3", "c5"):
         # c5: the last launch of the step covered the window's first
         # `counts[-1]` packets; check the whole window result of that launch
-        L, stride = shape
+        L, stride, at = shape
         n_chk = got.size if args.config != "c5" else min(got.size, last_count(args))
-        want = c_oracle.cksum_strided(hb, stride, L, n_chk, kind=k)
+        want = c_oracle.cksum_strided(hb, stride, L, n_chk, kind=k, byte_offset=at)
         got = got[:n_chk]
-        offs = np.arange(n_chk, dtype=np.uint64) * np.uint64(stride)
+        offs = np.arange(n_chk, dtype=np.uint64) * np.uint64(stride) + np.uint64(at)
     else:
         offs, lens = shape
         want = c_oracle.cksum_ragged(hb, offs, lens, kind=k)
@@ -677,6 +690,8 @@ def traffic_entry(args, meta, path):
     except (OSError, ValueError):
         return None, None
     key = f"{args.config}:{meta.get('packet_bytes', 'zipf')}"
+    if "stride" in meta:
+        key += f":s{meta['stride']}+{meta['offset']}"
     if args.kind != "ip" and args.config not in ("rx", "zrx"):
         key += f":{args.kind}"
     if args.headers and args.config not in ("rx", "zrx"):

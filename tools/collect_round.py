@@ -27,8 +27,9 @@ def main():
     go, prof = ROOT / "gpurun_out", ROOT / "profiles"
     traffic = json.loads((prof / "traffic.json").read_text())
     for c in cfgs:
-        key = KEYS.get(c) or "c3:" + c.split("_", 1)[1] + (":payload:headers"
-                                                           if c.startswith("c3pl_") else "")
+        L = c.split("_", 1)[-1]
+        key = KEYS.get(c) or ("c3:" + L + (":s2048+14" if c.startswith("s14") else "")
+                              + (":payload:headers" if c.startswith(("c3pl_", "s14pl_")) else ""))
         shutil.copy(go / "round" / f"bench_{tag}_{c}.json", prof / f"bench_{rnd}_{c}.json")
         shutil.copy(go / f"prof_{tag}_{c}" / "stats" / "run_kernel_stats.csv",
                     prof / f"rocprof_{rnd}_{c}_kernel_stats.csv")

@@ -28,6 +28,8 @@ for c in ${CFGS:-c2 c4 c4pl slotspl}; do
         rx) a="--config rx" ;;
         zrx) a="--config zrx" ;;
         c3pl_*) a="--config c3 --len ${c#c3pl_} --kind payload --headers" ;;
+        s14_*) a="--config c3 --len ${c#s14_} --stride 2048 --offset 14" ;;
+        s14pl_*) a="--config c3 --len ${c#s14pl_} --stride 2048 --offset 14 --kind payload --headers" ;;
         *) echo "unknown config $c"; exit 2 ;;
     esac
     echo "== $c: bench"
@@ -36,5 +38,5 @@ for c in ${CFGS:-c2 c4 c4pl slotspl}; do
         2> gpurun_out/round/bench_${TAG}_$c.err || { tail gpurun_out/round/bench_${TAG}_$c.err; exit 1; }
     cat gpurun_out/round/bench_${TAG}_$c.json
     echo "== $c: rocprof"
-    TAG=${TAG}_$c BENCH_ARGS="$a --steps 50 --warmup 5 --no-cpu-baseline --no-c5 --no-extra" tools/profile.sh || exit 1
+    TAG=${TAG}_$c BENCH_ARGS="$a --steps 50 --warmup 5 --no-cpu-baseline --no-c5 --no-extra --graph off" tools/profile.sh || exit 1
 done
