@@ -142,9 +142,14 @@ struct Config {
     int serve_waves = 64;          // WC_SERVE_WAVES: its waves (one 64-lane workgroup each)
     int serve_max = 256;           // WC_SERVE_MAX: largest batch (packets) it takes
     int serve_idle_us = 20000;     // WC_SERVE_IDLE_US: stopped after this long without a call
-    int rx_rows = 4;               // WC_RX_ROWS: RX verdict stream rows per group (2, 4)
     int rx_early = 0;              // WC_RX_EARLY: RX verdict parses before streaming
-    int rx_mode() const { return (rx_rows == 2 ? wc::kRxRows2 : 0) | (rx_early ? wc::kRxEarly : 0); }
+    int rx_hdrt = 1;               // WC_RX_HDRT: RX verdict header chunks loaded transposed
+    int rx_skip = 1;               // WC_RX_SKIP: frames the parse rules out leave the stream
+    int rx_mode() const
+    {
+        return (rx_early ? wc::kRxEarly : 0) | (rx_hdrt ? wc::kRxHdrT : 0) |
+               (rx_skip ? wc::kRxSkip : 0);
+    }
 };
 
 std::mutex g_mu;
@@ -224,8 +229,9 @@ void load_config_locked()
     c.serve_waves = std::max(1, std::min(env_int("WC_SERVE_WAVES", c.serve_waves), 1024));
     c.serve_max = std::max(0, std::min(env_int("WC_SERVE_MAX", c.serve_max), (int)wc::kSrvMaxPkts));
     c.serve_idle_us = std::max(100, env_int("WC_SERVE_IDLE_US", c.serve_idle_us));
-    c.rx_rows = env_int("WC_RX_ROWS", c.rx_rows);
     c.rx_early = env_int("WC_RX_EARLY", c.rx_early);
+    c.rx_hdrt = env_int("WC_RX_HDRT", c.rx_hdrt);
+    c.rx_skip = env_int("WC_RX_SKIP", c.rx_skip);
     g_cfg = c;
     g_cfg_loaded = true;
 }

@@ -165,9 +165,10 @@ hipError_t launch_synth(void *buf, uint64_t nbytes, uint64_t seed, int grid,
                         hipStream_t st);
 // RX verdicts of Ethernet frames [base + offs[i], + flens[i]) (wc_k_rx.hip);
 // drops (optional) accumulates the frames the reference's RX path drops.
-// mode: kRxRows2 (2-row stream groups instead of 4) | kRxEarly (parse, then
-// stream only the checked frames); every mode gives the same verdicts.
-constexpr int kRxRows2 = 1, kRxEarly = 2;
+// mode: kRxEarly (parse, then stream only the checked frames) | kRxHdrT
+// (transposed header loads) | kRxSkip (frames the parse rules out leave the
+// stream); every mode gives the same verdicts.
+constexpr int kRxEarly = 2, kRxHdrT = 4, kRxSkip = 8;
 hipError_t launch_rx_verdict(const void *base, const uint64_t *offs, const uint16_t *flens,
                              uint64_t n, uint8_t *verdict, uint64_t *drops, bool nt,
                              hipStream_t st, int mode = 0);

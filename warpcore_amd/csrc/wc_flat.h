@@ -63,7 +63,11 @@ __device__ __forceinline__ void wave_order()
 // slot is PK consecutive 16-byte chunks of one packet (PK = 2: every lane
 // streams 32 contiguous bytes per row, and the owner lookup, scan and
 // hand-offs below are paid once per 2 chunks).
-template <int UN, bool NT, bool NOLOAD = false, int PK = 1, int KIND = WC_KIND_IP>
+// SKIP: a descriptor whose info has bit 31 set is skipped -- its slots read
+// the zero chunk (the RX verdict kernel marks frames its header parse rules
+// out after the first row group is in flight).
+template <int UN, bool NT, bool NOLOAD = false, int PK = 1, int KIND = WC_KIND_IP,
+          bool SKIP = false>
 __device__ __forceinline__ void flat_issue(FlatRows<UN, PK> &R, FlatLds<UN> &L,
                                            uint32_t g0, int lane, uint32_t cp,
                                            uint32_t ce, uint32_t rank,
@@ -98,7 +102,12 @@ __device__ __forceinline__ void flat_issue(FlatRows<UN, PK> &R, FlatLds<UN> &L,
         // chunk and are zeroed in flat_accum): a straight-line issue stream
         // lets hipcc wait for exactly the older row group.
         const uint32_t q = min(row0 + (uint32_t)lane, total - 1u);
-        if constexpr (PK == 1) {
+        if constexpr (PK == 1 && SKIP) {
+            const FlatDesc g = L.desc[own];
+            const uint64_t vb = (uint64_t)g.vb_lo | ((uint64_t)g.vb_hi << 32);
+            R.d[u][0] = load_chunk<NT>((g.info >> 31) ? (uint64_t)(uintptr_t)&kZeroChunk
+                                                       : vb + 16ull * q);
+        } else if constexpr (PK == 1) {
             const uint64_t vb = *reinterpret_cast<const uint64_t *>(&L.desc[own]);
             if constexpr (NOLOAD) // diagnostic build: same stream, no HBM traffic
                 R.d[u][0] = u32x4{(uint32_t)vb, q, (uint32_t)(vb >> 32), q ^ 0x5a5a5a5au};

@@ -159,6 +159,46 @@ __device__ __forceinline__ void rx_load(uint64_t fa, uint32_t flen, bool valid, 
         c[k] = load_chunk<false>(valid && cf + 16ull * k < fend ? cf + 16ull * k : zero);
 }
 
+// The same five chunks, loaded transposed (HT): instruction i reads frames
+// 16 i .. 16 i + 15, four lanes per frame, lane 4 f' + j its chunk j -- 64
+// contiguous bytes per frame, one cache line instead of four separate
+// 16-byte requests (five one-lane-per-frame loads put 320 line requests per
+// tile in front of the stream's ~140).  Chunk 4 (frame bytes past 64 - sf)
+// is loaded per lane, and only by lanes whose start phase sf > 2 may need it
+// (the parse reads frame bytes < 14 + 40 + 8 = 62).  rx_hdr_gather then hands
+// each lane its frame's chunks through LDS.
+__device__ __forceinline__ void rx_load_t(uint64_t fa, uint32_t flen, bool valid, uint64_t zero,
+                                          int lane, u32x4 (&hx)[4], u32x4 &c4)
+{
+    const uint32_t lv = valid ? flen : 0u;
+    const uint64_t j16 = 16ull * (uint32_t)(lane & 3);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int f = 16 * i + (lane >> 2);
+        const uint64_t faf = (uint64_t)(uint32_t)__shfl((int)(uint32_t)fa, f, 64) |
+                             ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(fa >> 32), f, 64) << 32);
+        const uint32_t lf = (uint32_t)__shfl((int)lv, f, 64);
+        const uint64_t a = (faf & ~15ull) + j16;
+        hx[i] = load_chunk<false>(lf != 0u && a < faf + lf ? a : zero);
+    }
+    const uint64_t a4 = (fa & ~15ull) + 64u;
+    c4 = load_chunk<false>(lv != 0u && (fa & 15u) > 2u && a4 < fa + lv ? a4 : zero);
+}
+
+__device__ __forceinline__ void rx_hdr_gather(u32x4 *stage, int lane, const u32x4 (&hx)[4],
+                                              const u32x4 &c4, u32x4 (&c)[5])
+{
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        stage[64 * i + lane] = hx[i]; // frame 16 i + lane / 4, chunk lane % 4
+    wave_order();
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+        c[k] = stage[4 * lane + k];
+    c[4] = c4;
+    wave_order(); // stage is rewritten by the stream's first row group
+}
+
 __device__ __forceinline__ RxParse rx_parse(const u32x4 (&c)[5], uint64_t fa, uint32_t flen,
                                             bool valid, bool &slow)
 {
@@ -230,23 +270,29 @@ __device__ __forceinline__ RxParse rx_parse_slow(uint64_t fa, uint32_t flen, boo
 }
 
 
-// UNS: 64-chunk rows per row group of the gathered stream (4, as the seg
-// kernel's ragged default; 2 halves the rows in flight and the registers).
-// EARLY: the header parse completes BEFORE the stream, which then carries
-// only the frames that need the UDP check and only their checked range
-// [ip, ip + udp_len + hl) -- one load round trip per tile more, no bytes read
-// for frames the headers rule out (non-IP, non-UDP, bad IPv4 header,
-// fragments, zero UDP checksums); !EARLY streams every frame with >= 28 IP
-// bytes while the parse is in flight.
-template <int UNS, bool NT, bool EARLY>
+// One 64-chunk row group of 4 rows for the gathered stream (the seg
+// kernel's ragged default; 2-row groups measured slower, 128 -> 131 us on the
+// mixed ring: profiles/ab_r04_rx_modes.log).  Kernel modes (launch_rx_verdict),
+// all giving the same verdicts:
+//   EARLY  the header parse completes BEFORE the stream, which then carries
+//          only the frames that need the UDP check and only their checked
+//          range [ip, ip + udp_len + hl) -- one load round trip per tile
+//          more; otherwise every frame with >= 28 IP bytes starts streaming
+//          while the parse is in flight;
+//   HT     the header chunks are loaded transposed (rx_load_t);
+//   SKIP   (with !EARLY) once parsed, frames that need no check leave the
+//          stream: its later row groups read the zero chunk for them.
+template <bool NT, bool EARLY, bool HT, bool SKIP>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
 k_rx_verdict(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
              const uint16_t *__restrict__ flens, uint64_t n, uint8_t *__restrict__ verdict,
              unsigned long long *__restrict__ drops)
 {
+    constexpr int UNS = 4;
+    using Src = GathSrc<UNS, NT, SKIP && !EARLY>;
     struct Lds {
         FlatLds<UNS> f; // slot table, row marks, prefix sums
-        u32x4 stage[64 * UNS];
+        u32x4 stage[64 * UNS]; // also the header chunks' transpose (HT)
         u32x4 pm[17]; // seg_head's masks
     };
     __shared__ Lds lds_all[kFlatWaves];
@@ -273,12 +319,21 @@ k_rx_verdict(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
         meta_load(offs, flens, (tile + nwaves) * 64 + lane, n, off_n, flen_n);
 
         u32x4 c[5];
-        rx_load(fa, flen, valid, zero, c);
+        u32x4 hx[4], c4;
+        if constexpr (HT)
+            rx_load_t(fa, flen, valid, zero, lane, hx, c4);
+        else
+            rx_load(fa, flen, valid, zero, c);
+        auto headers = [&] { // this lane's frame chunks 0..4 (HT: through LDS)
+            if constexpr (HT)
+                rx_hdr_gather(L.stage, lane, hx, c4, c);
+        };
         const uint64_t ip = fa + 14u;
         bool slow = false;
         RxParse h{};
         uint32_t v;
         if constexpr (EARLY) {
+            headers();
             h = rx_parse(c, fa, flen, valid, slow);
             v = h.verdict;
             const bool need = h.need && !slow;
@@ -286,9 +341,9 @@ k_rx_verdict(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
                 const FlatTile t = flat_tile_setup<UNS, 1>(L.f, lane, ip, h.plen, h.plen, need, 0u);
                 bool done = true;
                 uint16_t rh = 0;
-                uint16_t r = seg_tile<UNS, WC_KIND_PAYLOAD, NT, false, GathSrc<UNS, NT>, true>(
+                uint16_t r = seg_tile<UNS, WC_KIND_PAYLOAD, NT, false, Src, true>(
                     L.f.pre, L.stage, L.pm, lane, ip, 16ull * t.cp + (ip & 15u), h.plen, need,
-                    t.total, GathSrc<UNS, NT>{&L.f, t}, zero, done, rh);
+                    t.total, Src{&L.f, t}, zero, done, rh);
                 if (need && !done) // header longer than the packet, or a possible wrap
                     r = lane_payload_exact<NT>(ip, h.plen);
                 if (need)
@@ -301,25 +356,30 @@ k_rx_verdict(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
             // the seg path's gathered stream, and the parse completes once
             // that stream's first row group is in flight (seg_tile's Late
             // hook): the checked range [ip, ip + udp_len + hl) is a prefix of
-            // the streamed one.  Frames that turn out not to need the check
-            // were read for nothing.
+            // the streamed one.  A frame that turns out not to need the check
+            // was read for the first row group only (SKIP).
             const uint32_t room = flen >= 14u ? flen - 14u : 0u;
             const bool spec = valid && room >= 28u;
             if (__ballot(spec)) {
                 const FlatTile t = flat_tile_setup<UNS, 1>(L.f, lane, ip, room, room, spec, 0u);
                 bool need = false;
                 auto late = [&](uint32_t &len, bool &on) {
+                    headers();
                     h = rx_parse(c, fa, flen, valid, slow);
                     need = h.need && !slow;
                     on = need;
                     len = need ? h.plen : 0u;
+                    if constexpr (SKIP) {
+                        if (spec && !need) // its later chunks: the zero chunk
+                            L.f.desc[t.rank].info = 1u << 31;
+                        wave_order();
+                    }
                 };
                 bool done = true;
                 uint16_t rh = 0;
-                uint16_t r = seg_tile<UNS, WC_KIND_PAYLOAD, NT, false, GathSrc<UNS, NT>, true,
-                                      decltype(late)>(
+                uint16_t r = seg_tile<UNS, WC_KIND_PAYLOAD, NT, false, Src, true, decltype(late)>(
                     L.f.pre, L.stage, L.pm, lane, ip, 16ull * t.cp + (ip & 15u), room, spec,
-                    t.total, GathSrc<UNS, NT>{&L.f, t}, zero, done, rh, late);
+                    t.total, Src{&L.f, t}, zero, done, rh, late);
                 if (need && !done) // header longer than the packet, or a possible wrap
                     r = lane_payload_exact<NT>(ip, h.plen);
                 v = h.verdict;
@@ -327,6 +387,7 @@ k_rx_verdict(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
                     v = r != 0 ? kRxBadUdpCksum : kRxOk; // udp.c:134-139
                 wave_order(); // the tables are rewritten by the next tile
             } else {
+                headers();
                 h = rx_parse(c, fa, flen, valid, slow);
                 v = h.verdict;
             }
@@ -352,6 +413,17 @@ k_rx_verdict(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
 
 } // namespace
 
+template <bool NT, bool EARLY, bool HT, bool SKIP>
+static hipError_t launch_rx_one(const void *base, const uint64_t *offs, const uint16_t *flens,
+                                uint64_t n, uint8_t *verdict, uint64_t *drops, int grid,
+                                hipStream_t st)
+{
+    hipLaunchKernelGGL((k_rx_verdict<NT, EARLY, HT, SKIP>), dim3(grid), dim3(256), 0, st,
+                       (const uint8_t *)base, offs, flens, n, verdict,
+                       (unsigned long long *)drops);
+    return hipGetLastError();
+}
+
 hipError_t launch_rx_verdict(const void *base, const uint64_t *offs, const uint16_t *flens,
                              uint64_t n, uint8_t *verdict, uint64_t *drops, bool nt,
                              hipStream_t st, int mode)
@@ -359,24 +431,20 @@ hipError_t launch_rx_verdict(const void *base, const uint64_t *offs, const uint1
     const uint64_t tiles = (n + 63) / 64;
     const int grid = (int)std::min<uint64_t>(
         kMaxGridBlocks, std::max<uint64_t>(1, (tiles + kFlatWaves - 1) / kFlatWaves));
-    const bool rows2 = (mode & kRxRows2) != 0, early = (mode & kRxEarly) != 0;
-#define WC_RX_LAUNCH(U, N, E)                                                  \
-    hipLaunchKernelGGL((k_rx_verdict<U, N, E>), dim3(grid), dim3(256), 0, st,  \
-                       (const uint8_t *)base, offs, flens, n, verdict,         \
-                       (unsigned long long *)drops)
-    const int sel = (nt ? 4 : 0) | (rows2 ? 2 : 0) | (early ? 1 : 0);
-    switch (sel) {
-    case 7: WC_RX_LAUNCH(2, true, true); break;
-    case 6: WC_RX_LAUNCH(2, true, false); break;
-    case 5: WC_RX_LAUNCH(4, true, true); break;
-    case 4: WC_RX_LAUNCH(4, true, false); break;
-    case 3: WC_RX_LAUNCH(2, false, true); break;
-    case 2: WC_RX_LAUNCH(2, false, false); break;
-    case 1: WC_RX_LAUNCH(4, false, true); break;
-    default: WC_RX_LAUNCH(4, false, false); break;
-    }
-#undef WC_RX_LAUNCH
-    return hipGetLastError();
+    const bool early = mode & kRxEarly, ht = mode & kRxHdrT, skip = mode & kRxSkip;
+#define WC_RX(N, E, H, S)                                                      \
+    if (nt == N && early == E && ht == H && skip == S)                         \
+        return launch_rx_one<N, E, H, S>(base, offs, flens, n, verdict, drops, grid, st);
+#define WC_RX_NT(N)                                                            \
+    WC_RX(N, false, false, false) WC_RX(N, false, false, true)                 \
+    WC_RX(N, false, true, false) WC_RX(N, false, true, true)                   \
+    WC_RX(N, true, false, false) WC_RX(N, true, true, false)
+    WC_RX_NT(true)
+    WC_RX_NT(false)
+#undef WC_RX_NT
+#undef WC_RX
+    // EARLY streams only the checked frames: SKIP has nothing to skip
+    return launch_rx_one<true, true, true, false>(base, offs, flens, n, verdict, drops, grid, st);
 }
 
 } // namespace wc

@@ -272,7 +272,7 @@ struct DenseSrc {
     }
 };
 
-template <int UNS, bool NT>
+template <int UNS, bool NT, bool SKIP = false>
 struct GathSrc {
     static constexpr bool kClamp = true;
     FlatLds<UNS> *L;
@@ -280,7 +280,8 @@ struct GathSrc {
     __device__ __forceinline__ void issue(SegRows<UNS> &R, uint32_t g0, int lane) const
     {
         FlatRows<UNS, 1> F;
-        flat_issue<UNS, NT>(F, *L, g0, lane, t.cp, t.ce, t.rank, t.last_rank, t.total);
+        flat_issue<UNS, NT, false, 1, WC_KIND_IP, SKIP>(F, *L, g0, lane, t.cp, t.ce, t.rank,
+                                                        t.last_rank, t.total);
 #pragma unroll
         for (int u = 0; u < UNS; ++u)
             R.d[u] = F.d[u][0];
