@@ -128,7 +128,9 @@ def test_bench_other_configs(gpu, args):
     assert r.returncode == 0, r.stderr[-2000:]
     line = _last_json(r.stdout)
     assert line["value"] > 0 and line["parity"]["mismatches"] == 0
-    assert line["parity"]["checked_packets"] == line["config"]["packets_per_gpu"]
+    # strided batches smaller than 1 GiB rotate over K distinct batches, each checked
+    K = line["config"].get("batches", 1)
+    assert line["parity"]["checked_packets"] == line["config"]["packets_per_gpu"] * K
 
 
 def test_bench_spawns_ranks_without_torchrun(gpu):
