@@ -141,7 +141,7 @@ def test_bench_spawns_ranks_without_torchrun(gpu):
     env["WC_DIST_BACKEND"] = "gloo"
     r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "2",
                         "--steps", "5", "--warmup", "1", "--packets", "65536", "--no-c5",
-                        "--no-cpu-baseline", "--no-extra"],
+                        "--no-cpu-baseline", "--no-extra", "--batches", "1"],
                        capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     line = _last_json(r.stdout)
