@@ -495,37 +495,6 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t v)
     return lane_u32(v, 63);
 }
 
-// Block-delegated result stores for one-shot grids (every wave of a
-// 256-thread block does one iteration).  A wave ends only once its stores are
-// acknowledged, so a store at the end of every wave adds its completion
-// latency to every wave's lifetime: C4 took 615 us with its result stores and
-// 585 us without, ~300 cycles more per wave, with full 64-byte write requests
-// and no write stalls at the memory side (profiles/pmc_r04_c4_store.txt).
-// Instead each wave parks its results in LDS and the block's last wave to
-// arrive writes all of them.  `arrive` must be 0 before any wave arrives
-// (block_store_init + one __syncthreads at kernel start).
-__device__ __forceinline__ void block_store_init(uint32_t *arrive)
-{
-    if (threadIdx.x == 0)
-        *arrive = 0u;
-    __syncthreads();
-}
-
-// true in every lane of the block's last wave to arrive (after its parked
-// results are visible to it).
-__device__ __forceinline__ bool block_store_last(uint32_t *arrive, int lane)
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    uint32_t prev = 0;
-    if (lane == 0)
-        prev = atomicAdd(arrive, 1u);
-    prev = (uint32_t)__builtin_amdgcn_readfirstlane((int)prev);
-    if (prev != (blockDim.x >> 6) - 1u)
-        return false;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-    return true;
-}
-
 // Packet p's offset and length, or packet 0's offset and length 0 past the
 // batch end -- with unconditional loads.
 __device__ __forceinline__ void meta_load(const uint64_t *__restrict__ offs,

@@ -79,16 +79,8 @@ k_cksum_lean(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len, ui
     const uint32_t lo = grp * (uint32_t)stride + 16u * gl;
     const uint32_t ustep = (uint32_t)GPW * (uint32_t)stride;
     uint32_t nbad = 0;
-    // One-shot grid: results through LDS to the block's last wave
-    // (block_store_last, wc_device.h).
-    __shared__ uint16_t res_blk[4 * PPW];
-    __shared__ uint32_t arrive;
-    const uint64_t wave0 = xcd_block(variant) * 4u;
-    const bool one_shot = nwaves * PPW >= n;
-    if (one_shot)
-        block_store_init(&arrive);
 
-    for (uint64_t wave = wave0 + wib; wave * PPW < n; wave += nwaves) {
+    for (uint64_t wave = xcd_block(variant) * 4u + wib; wave * PPW < n; wave += nwaves) {
         const uint64_t p0 = wave * PPW;
         const gbyte_ptr gb = (gbyte_ptr)(base + p0 * stride);
         u32x4 d[U][CPL];
@@ -166,19 +158,9 @@ k_cksum_lean(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len, ui
             if constexpr (PL)
                 if (res >> 16) // IPv4 header with options / IHL < 5: exact, by this lane
                     r = lane_payload_exact<NT>((uint64_t)base + i * stride, len);
-            if (one_shot)
-                res_blk[wib * PPW + (uint32_t)lane] = r;
-            else if (out)
+            if (out)
                 out[i] = r;
             nbad += r != 0;
-        }
-    }
-    if (one_shot && block_store_last(&arrive, lane) && out) {
-#pragma unroll
-        for (uint32_t k = (uint32_t)lane; k < 4u * PPW; k += 64u) {
-            const uint64_t q = wave0 * PPW + k;
-            if (q < n)
-                out[q] = res_blk[k];
         }
     }
     if (bad) {

@@ -296,8 +296,6 @@ k_rx_verdict(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
         u32x4 pm[17]; // seg_head's masks
     };
     __shared__ Lds lds_all[kFlatWaves];
-    __shared__ uint8_t res_blk[kFlatWaves * 64]; // one-shot grid: the block's verdicts
-    __shared__ uint32_t arrive;
 
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); // wave-uniform: SGPR
@@ -305,16 +303,9 @@ k_rx_verdict(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
     seg_init_masks(L.pm, lane); // read after the first row group's wave_order
     const uint64_t ntiles = (n + 63) / 64;
     const uint64_t nwaves = (uint64_t)gridDim.x * kFlatWaves;
-    const uint64_t tile0 = xcd_block(13 << 8) * kFlatWaves; // the seg kernel's XCD span
-    uint64_t tile = tile0 + w;
+    uint64_t tile = xcd_block(13 << 8) * kFlatWaves + w; // the seg kernel's XCD span
     uint32_t ndrop = 0;
     const uint64_t zero = (uint64_t)(uintptr_t)&kZeroChunk;
-    // One tile per wave (one-shot grid): the verdicts go through LDS to the
-    // block's last wave to finish, the only one whose lifetime then includes
-    // a store's completion (k_cksum_seg, block_store).
-    const bool one_shot = nwaves >= ntiles;
-    if (one_shot)
-        block_store_init(&arrive);
 
     uint64_t off_n;
     uint32_t flen_n;
@@ -409,21 +400,9 @@ k_rx_verdict(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
                     v = lane_payload_exact<NT>(hs.ip, hs.plen) != 0 ? kRxBadUdpCksum : kRxOk;
             }
         }
-        if (one_shot)
-            res_blk[64 * w + lane] = (uint8_t)v;
-        else if (valid)
+        if (valid)
             verdict[p] = (uint8_t)v;
         ndrop += valid && rx_is_drop(v);
-    }
-    if (one_shot && block_store_last(&arrive, lane)) {
-        {
-#pragma unroll
-            for (int k = 0; k < kFlatWaves; ++k) {
-                const uint64_t q = (tile0 + k) * 64 + lane;
-                if (q < n)
-                    verdict[q] = res_blk[64 * k + lane];
-            }
-        }
     }
     if (drops) {
         ndrop = group_sum<64>(ndrop);

@@ -52,11 +52,6 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     using TileLds = typename std::conditional<kSegOnly, SegOnlyLds, FullLds>::type;
     __shared__ TileLds lds_all[kFlatWaves];
     __shared__ u32x4 head_masks[kFlatWaves][17]; // seg_head's tables, one per wave
-    // One-shot grid: the block's results are parked here and written by the
-    // block's last wave to finish (block_store).
-    __shared__ uint16_t res_blk[kFlatWaves * 64];
-    __shared__ uint16_t resh_blk[HDR ? kFlatWaves * 64 : 1];
-    __shared__ uint32_t arrive;
 
     const int lane = threadIdx.x & 63;
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); // wave-uniform: SGPR
@@ -69,18 +64,9 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
     // sets the span: +0.5-1 point on C4, the mixed ring and packed 300 B over
     // the strided kernel's 2^12 (profiles/ab_r02_xcd_span.log).
     const int xv = (variant & 0xFF00) ? variant : (variant | (13 << 8));
-    const uint64_t tile0 = xcd_block(xv) * kFlatWaves; // the block's first tile
-    uint64_t tile = tile0 + w;
+    uint64_t tile = xcd_block(xv) * kFlatWaves + w;
     uint32_t nbad = 0;
     const uint64_t zero = (uint64_t)(uintptr_t)&kZeroChunk;
-    // Each wave's tile is its only one (the default one-shot grid): results go
-    // through LDS to the block's last wave, so only that wave's lifetime
-    // includes a store's completion (a wave ends only when its stores are
-    // acknowledged: C4 with its result stores took 615 us, without them 585,
-    // ~300 more cycles per wave -- profiles/pmc_r04_c4_store.txt).
-    const bool one_shot = (uint64_t)gridDim.x * kFlatWaves >= ntiles;
-    if (one_shot)
-        block_store_init(&arrive);
 
     // Unconditional metadata prefetch loads, as in k_cksum_flat.  No header
     // prefetch: the seg path reads payload_cksum's header bytes out of its
@@ -198,11 +184,7 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
         // (Tuning build only, for the write-cost counters of DESIGN.md
         // section 10: WC_VARIANT bit 24 drops the result store, bit 25 the
         // header-checksum store -- results are then missing.)
-        if (one_shot) {
-            res_blk[64 * w + lane] = r;
-            if constexpr (HDR)
-                resh_blk[64 * w + lane] = rh;
-        } else if (valid) {
+        if (valid) {
             if constexpr (HDR)
                 if (!(variant & (1 << 25)))
                     out_hdr[p] = rh;
@@ -211,23 +193,6 @@ k_cksum_seg(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
         }
         nbad += valid && r != 0;
         wave_order(); // the tables are rewritten by the next tile
-    }
-    // The block's last wave to arrive stores its 256 packets' results: four
-    // coalesced 128-byte stores per array.
-    if (one_shot && block_store_last(&arrive, lane)) {
-        {
-#pragma unroll
-            for (int k = 0; k < kFlatWaves; ++k) {
-                const uint64_t q = (tile0 + k) * 64 + lane;
-                if (q < n) {
-                    if constexpr (HDR)
-                        if (!(variant & (1 << 25)))
-                            out_hdr[q] = resh_blk[64 * k + lane];
-                    if (out && !(variant & (1 << 24)))
-                        out[q] = res_blk[64 * k + lane];
-                }
-            }
-        }
     }
     if (bad) {
         nbad = group_sum<64>(nbad);

@@ -71,17 +71,6 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
     // WC_VARIANT bit 128 keeps the leader stores (A/B).
     constexpr bool kLaneStore = PPW <= 64;
     const bool lane_store = kLaneStore && !(variant & 128);
-    // One-shot grid with lane stores: the results go through LDS to the
-    // block's last wave (block_store_last, wc_device.h), so only one wave of
-    // four waits for a store's completion before it ends.
-    constexpr uint32_t kBlk = kLaneStore ? 4u * (uint32_t)PPW : 1u;
-    __shared__ uint16_t res_blk[kBlk];
-    __shared__ uint16_t resh_blk[HDR ? kBlk : 1u];
-    __shared__ uint32_t arrive;
-    const uint64_t wave0 = xcd_block(variant) * (blockDim.x >> 6);
-    const bool blk_store = lane_store && nwaves * PPW >= n;
-    if (blk_store)
-        block_store_init(&arrive);
 
     for (uint64_t p0 = wave * PPW; p0 < n; p0 += nwaves * PPW) {
         uint32_t res = 0, res_h = 0;
@@ -259,29 +248,11 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
             const uint64_t i = p0 + (uint64_t)lane;
             if (lane < (int)PPW && i < n) {
                 const uint16_t r = (uint16_t)res;
-                if (blk_store) {
-                    const uint32_t k = (uint32_t)(threadIdx.x >> 6) * (uint32_t)PPW + (uint32_t)lane;
-                    res_blk[k] = r;
-                    if constexpr (HDR)
-                        resh_blk[k] = (uint16_t)res_h;
-                } else {
-                    if (out && !(variant & 64)) // WC_VARIANT bit 64: no result store (timing only)
-                        out[i] = r; // (a nontemporal store measured the same)
-                    if constexpr (HDR)
-                        out_hdr[i] = (uint16_t)res_h; // ip4.c:110-115
-                }
+                if (out && !(variant & 64)) // WC_VARIANT bit 64: no result store (timing only)
+                    out[i] = r; // (a nontemporal store measured the same)
                 nbad += r != 0;
-            }
-        }
-    }
-    if (blk_store && block_store_last(&arrive, lane)) {
-        for (uint32_t k = (uint32_t)lane; k < kBlk; k += 64u) {
-            const uint64_t q = wave0 * PPW + k;
-            if (q < n) {
-                if (out && !(variant & 64))
-                    out[q] = res_blk[k];
                 if constexpr (HDR)
-                    out_hdr[q] = resh_blk[k]; // ip4.c:110-115
+                    out_hdr[i] = (uint16_t)res_h; // ip4.c:110-115
             }
         }
     }
