@@ -6,8 +6,12 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 O=gpurun_out/r04d
 mkdir -p $O
 export TMPDIR=/tmp WC_NO_BUILD=1
-timeout -k 10 300 python -u -m pytest tests/test_gpu_rx.py -x -q --timeout 300 --timeout-method thread -k "early" > $O/t_rx.log 2>&1 || { tail -30 $O/t_rx.log; exit 1; }
+timeout -k 10 400 python -u -m pytest tests/test_gpu_rx.py tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "early or host_ or rx_verdict_host or c_rx or c_host" > $O/t_rx.log 2>&1 || { tail -30 $O/t_rx.log; exit 1; }
 tail -1 $O/t_rx.log
+for W in 64 128; do
+  WC_SERVE_WAVES=$W timeout -k 10 200 build/host_latency 16 0.2 > $O/host_latency_w$W.log 2>&1 || { tail $O/host_latency_w$W.log; exit 1; }
+  echo "== waves $W"; cut -c1-150 $O/host_latency_w$W.log | head -4; sed -n 7,10p $O/host_latency_w$W.log | cut -c1-150
+done
 T="python tools/tune.py --rounds 4 --iters 20 --warm-ms 50"
 for a in "--config zrx" "--config rx" "--config zrx --rx-arp 3"; do
   echo "== $a" | tee -a $O/ab.log

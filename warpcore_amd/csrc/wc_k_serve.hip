@@ -60,7 +60,12 @@ struct Rec {
 
 __device__ __forceinline__ Rec rec_load(const SrvRec *r)
 {
-    const u32x4 v = load_sys16(r);
+    u32x4 v = load_sys16(r);
+    // every lane loaded the same record: make it wave-uniform (SGPRs)
+    v.x = (uint32_t)__builtin_amdgcn_readfirstlane((int)v.x);
+    v.y = (uint32_t)__builtin_amdgcn_readfirstlane((int)v.y);
+    v.z = (uint32_t)__builtin_amdgcn_readfirstlane((int)v.z);
+    v.w = (uint32_t)__builtin_amdgcn_readfirstlane((int)v.w);
     Rec x;
     x.addr = (uint64_t)v.x | ((uint64_t)v.y << 32);
     x.len = v.z & 0xFFFFu;
@@ -84,13 +89,16 @@ __device__ __forceinline__ void sv_load(uint64_t a, uint32_t span, int lane, u32
     }
 }
 
-// Byte o of the packet from lane-held chunks (any lane may ask; wave-wide).
+// Byte o of the packet from lane-held chunks (o uniform and s + o < 1024:
+// the chunk sits in d[0] of lane (s + o) >> 4): one v_readlane, no LDS round
+// trip -- the RX parse reads a dozen header bytes one after the other.
 __device__ __forceinline__ uint32_t sv_byte(const u32x4 (&d)[kSvLoads], uint32_t s, uint32_t o)
 {
-    const uint32_t pos = s + o; // byte position in the chunk stream
-    const uint32_t k = pos >> 4;  // chunk index (< 64: inside d[0] of lane k)
-    const uint32_t dw = __shfl(pick_dword(d[0], (int)((pos >> 2) & 3u)), (int)k, 64);
-    return (dw >> (8u * (pos & 3u))) & 0xFFu;
+    const uint32_t pos = (uint32_t)__builtin_amdgcn_readfirstlane((int)(s + o));
+    const uint32_t j = (pos >> 2) & 3u;
+    const uint32_t dw = j == 0 ? d[0].x : j == 1 ? d[0].y : j == 2 ? d[0].z : d[0].w;
+    const uint32_t v = (uint32_t)__builtin_amdgcn_readlane((int)dw, (int)(pos >> 4));
+    return (v >> (8u * (pos & 3u))) & 0xFFu;
 }
 
 // Exact sum (reference accumulator, mod 2^32) of packet bytes [rs, re) --
@@ -110,14 +118,20 @@ __device__ __forceinline__ uint32_t sv_sum(const u32x4 (&d)[kSvLoads], uint32_t 
     return group_sum<64>(combine(E, O, odd));
 }
 
-// ip_cksum / payload_cksum of [a, a + len) (in_cksum.c:133-167).
-__device__ __forceinline__ uint32_t sv_cksum(uint64_t a, uint32_t len, uint32_t kind, int lane)
+// Bytes a packet's check reads: payload_cksum reads the IPv4 header fields
+// up to byte 19 whatever len is (in_cksum.c:149-151); an RX frame its length.
+__device__ __forceinline__ uint32_t sv_span(uint32_t len, uint32_t kind)
 {
-    u32x4 d[kSvLoads];
-    const bool pl = kind == WC_KIND_PAYLOAD;
-    sv_load(a, pl ? max(len, 20u) : len, lane, d); // payload_cksum reads the v4 header
-    const uint32_t s = (uint32_t)(a & 15u);
-    if (!pl)
+    return kind == WC_KIND_PAYLOAD ? max(len, 20u) : len;
+}
+
+// ip_cksum / payload_cksum of [a, a + len) (in_cksum.c:133-167) from its
+// loaded chunks.
+__device__ __forceinline__ uint32_t sv_cksum(const u32x4 (&d)[kSvLoads], uint64_t a, uint32_t len,
+                                             uint32_t kind, int lane)
+{
+    const uint32_t s = (uint32_t)__builtin_amdgcn_readfirstlane((int)(a & 15u));
+    if (kind != WC_KIND_PAYLOAD)
         return fold_not(sv_sum<WC_KIND_IP>(d, s, lane, 0, (int)len, 0u, a & 1u));
     const PseudoHdr ph =
         pseudo_hdr(sv_byte(d, s, 0), sv_byte(d, s, 2), sv_byte(d, s, 3), sv_byte(d, s, 6));
@@ -127,11 +141,10 @@ __device__ __forceinline__ uint32_t sv_cksum(uint64_t a, uint32_t len, uint32_t 
 
 // The RX verdict of frame [fa, fa + flen), the reference's check order
 // (oracle_rx_verdict, k_rx_verdict): only bytes inside the frame are used.
-__device__ __forceinline__ uint32_t sv_rx(uint64_t fa, uint32_t flen, int lane)
+__device__ __forceinline__ uint32_t sv_rx(const u32x4 (&d)[kSvLoads], uint64_t fa, uint32_t flen,
+                                          int lane)
 {
-    u32x4 d[kSvLoads];
-    sv_load(fa, flen, lane, d);
-    const uint32_t s = (uint32_t)(fa & 15u);
+    const uint32_t s = (uint32_t)__builtin_amdgcn_readfirstlane((int)(fa & 15u));
     auto B = [&](uint32_t o) { return sv_byte(d, s, o); };
     if (flen < 14u)
         return kSvTruncated;
@@ -209,19 +222,68 @@ __global__ void __launch_bounds__(64) k_serve(const SrvRec *__restrict__ recs,
         // caches), then the packets' bytes are read fresh from host memory.
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         const uint32_t seq = r.seq;
-        for (uint32_t k = w; k < kSrvMaxPkts; k += W) {
-            if (k != w)
-                r = rec_load(&recs[k]);
-            if (r.seq != seq)
-                break; // past the request's last packet
-            uint32_t v;
-            if (r.kind == kSrvKindRx)
-                v = sv_rx(r.addr, r.len, lane);
-            else
-                v = sv_cksum(r.addr, r.len, r.kind, lane);
-            if (lane == 0)
-                __hip_atomic_store((uint64_t *)&res[k], (uint64_t)v | ((uint64_t)seq << 32),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        // This wave's packets are w + j W, j = 0, 1, ...: their records are
+        // fetched 64 at a time in one load (lane i reads the record of packet
+        // j0 + 1 + i); the host wrote them all before record w, so they are
+        // current when w is.  Two packets are processed at a time, both
+        // packets' loads in flight before either is summed.
+        Rec r0 = r;
+        uint32_t j = 0;
+        for (bool more = true; more;) {
+            const uint32_t j0 = j; // r0 is packet j0's record
+            const uint32_t kx = w + (j0 + 1u + (uint32_t)lane) * W;
+            const u32x4 rv = load_sys16(&recs[kx < kSrvMaxPkts ? kx : w]);
+            auto rec_at = [&](uint32_t jj) { // packet jj's record, j0 < jj <= j0 + 64
+                Rec x;
+                const int l = (int)(jj - j0 - 1u);
+                x.addr = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)rv.x, l) |
+                         ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)rv.y, l) << 32);
+                const uint32_t z = (uint32_t)__builtin_amdgcn_readlane((int)rv.z, l);
+                x.len = z & 0xFFFFu;
+                x.kind = (z >> 16) & 0xFFu;
+                x.stop = z >> 24;
+                x.seq = w + jj * W < kSrvMaxPkts
+                            ? (uint32_t)__builtin_amdgcn_readlane((int)rv.w, l) : ~seq;
+                return x;
+            };
+            more = false;
+            while (r0.seq == seq) {
+                const bool last_in_batch = j == j0 + 64u; // r1 would need the next batch
+                const Rec r1 = last_in_batch ? Rec{0, 0, 0, 0, ~seq} : rec_at(j + 1u);
+                const bool two = r1.seq == seq;
+                u32x4 d0[kSvLoads], d1[kSvLoads];
+                sv_load(r0.addr, sv_span(r0.len, r0.kind), lane, d0);
+                if (two)
+                    sv_load(r1.addr, sv_span(r1.len, r1.kind), lane, d1);
+                auto answer = [&](const Rec &x, const u32x4 (&d)[kSvLoads], uint32_t k) {
+                    const uint32_t v = x.kind == kSrvKindRx
+                                           ? sv_rx(d, x.addr, x.len, lane)
+                                           : sv_cksum(d, x.addr, x.len, x.kind, lane);
+                    if (lane == 0)
+                        __hip_atomic_store((uint64_t *)&res[k],
+                                           (uint64_t)v | ((uint64_t)seq << 32), __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_SYSTEM);
+                };
+                answer(r0, d0, w + j * W);
+                if (last_in_batch) { // packet j + 1's record is in the next batch
+                    j += 1u;
+                    more = w + j * W < kSrvMaxPkts;
+                    if (more)
+                        r0 = rec_load(&recs[w + j * W]);
+                    break;
+                }
+                if (!two)
+                    break;
+                answer(r1, d1, w + (j + 1u) * W);
+                j += 2u;
+                if (j > j0 + 64u) { // both of packets j0 + 63, j0 + 64 done
+                    more = w + j * W < kSrvMaxPkts;
+                    if (more)
+                        r0 = rec_load(&recs[w + j * W]);
+                    break;
+                }
+                r0 = rec_at(j);
+            }
         }
         last = seq;
         t_last = (uint64_t)wall_clock64();
