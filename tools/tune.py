@@ -86,6 +86,9 @@ def main():
                     help="fused IPv4 header + payload_cksum pass (wc_cksum_ip_udp_*)")
     ap.add_argument("--headers", action="store_true",
                     help="well-formed IPv4 / IPv6 UDP headers (synth.stamp_udp_headers)")
+    ap.add_argument("--rotate-bytes", type=int, default=0,
+                    help="c2/c3: rotate the launches over ceil(B / batch) distinct buffers "
+                         "(HBM, not the 256 MiB Infinity Cache)")
     ap.add_argument("--rx-arp", type=int, default=0,
                     help="rx / zrx: every K-th frame an ARP frame (no UDP check)")
     ap.add_argument("--ragged", action="store_true",
@@ -144,14 +147,25 @@ def main():
         n = args.packets
         stride = args.stride or L
         nbytes = n * L
-        buf = torch.empty(args.offset + n * stride + 64, dtype=torch.uint8, device=dev)
-        wc.synth_fill(buf, 1)
-        if args.headers:
-            synth.stamp_udp_headers(buf, torch.arange(n, device=dev) * stride + args.offset,
-                                    torch.full((n,), L, device=dev))
+        K = max(1, -(-args.rotate_bytes // (args.offset + n * stride))) if args.rotate_bytes else 1
+        bufs = []
+        for k in range(K):
+            b = torch.empty(args.offset + n * stride + 64, dtype=torch.uint8, device=dev)
+            wc.synth_fill(b, 1 + k)
+            if args.headers:
+                synth.stamp_udp_headers(b, torch.arange(n, device=dev) * stride + args.offset,
+                                        torch.full((n,), L, device=dev))
+            bufs.append(b)
+        buf = bufs[0]
         out = torch.empty(n, dtype=torch.uint16, device=dev)
-        run = lambda: wc.cksum_strided(buf, stride, L, n, out=out, kind=args.kind,  # noqa: E731
-                                       byte_offset=args.offset)
+        rot = [0]
+
+        def run():
+            rot[0] = (rot[0] + 1) % K
+            wc.cksum_strided(bufs[rot[0]], stride, L, n, out=out, kind=args.kind,
+                             byte_offset=args.offset)
+        if K > 1:
+            print(f"rotating over {K} buffers", flush=True)
         if args.fused:
             run = lambda: wc.cksum_ip_udp_strided(buf, stride, L, n,  # noqa: E731
                                                   byte_offset=args.offset)

@@ -142,9 +142,13 @@ struct Config {
     int serve_waves = 64;          // WC_SERVE_WAVES: its waves (one 64-lane workgroup each)
     int serve_max = 256;           // WC_SERVE_MAX: largest batch (packets) it takes
     int serve_idle_us = 20000;     // WC_SERVE_IDLE_US: stopped after this long without a call
+    // RX verdict kernel modes (profiles/ab_r04_rx_*.log): transposed header
+    // loads win everywhere (mixed ring 127.5 -> 111.4 us); parsing first
+    // (EARLY) wins when many frames need no UDP check (a third ARP: 111.8 ->
+    // 96.6 us) and loses 3 us on an all-UDP ring; SKIP loses on all-UDP rings.
     int rx_early = 0;              // WC_RX_EARLY: RX verdict parses before streaming
     int rx_hdrt = 1;               // WC_RX_HDRT: RX verdict header chunks loaded transposed
-    int rx_skip = 1;               // WC_RX_SKIP: frames the parse rules out leave the stream
+    int rx_skip = 0;               // WC_RX_SKIP: frames the parse rules out leave the stream
     int rx_mode() const
     {
         return (rx_early ? wc::kRxEarly : 0) | (rx_hdrt ? wc::kRxHdrT : 0) |

@@ -282,11 +282,11 @@ __device__ __forceinline__ RxParse rx_parse_slow(uint64_t fa, uint32_t flen, boo
 //   HT     the header chunks are loaded transposed (rx_load_t);
 //   SKIP   (with !EARLY) once parsed, frames that need no check leave the
 //          stream: its later row groups read the zero chunk for them.
-#ifndef WC_RX_EARLY_WAVES
-#define WC_RX_EARLY_WAVES 5 // waves per SIMD the EARLY kernels are register-capped for
-#endif
+// (4 waves per SIMD for every mode: capping the EARLY kernels at 96 VGPRs
+// for 5 spilled 4 of them and took the mixed ring from 114 to 141 us,
+// profiles/ab_r04_rx_early_waves.log.)
 template <bool NT, bool EARLY, bool HT, bool SKIP>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EARLY ? WC_RX_EARLY_WAVES : 4)))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
 k_rx_verdict(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
              const uint16_t *__restrict__ flens, uint64_t n, uint8_t *__restrict__ verdict,
              unsigned long long *__restrict__ drops)

@@ -232,7 +232,15 @@ __global__ void __launch_bounds__(64) k_serve(const SrvRec *__restrict__ recs,
         for (bool more = true; more;) {
             const uint32_t j0 = j; // r0 is packet j0's record
             const uint32_t kx = w + (j0 + 1u + (uint32_t)lane) * W;
-            const u32x4 rv = load_sys16(&recs[kx < kSrvMaxPkts ? kx : w]);
+            // (two 8-byte system-scope loads the compiler waits for only at
+            // first use: in flight with packet j0's loads; records written
+            // before the one already seen need no single-snapshot load)
+            const uint64_t *rp = (const uint64_t *)&recs[kx < kSrvMaxPkts ? kx : w];
+            const uint64_t rlo = __hip_atomic_load(rp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            const uint64_t rhi =
+                __hip_atomic_load(rp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            const u32x4 rv = {(uint32_t)rlo, (uint32_t)(rlo >> 32), (uint32_t)rhi,
+                              (uint32_t)(rhi >> 32)};
             auto rec_at = [&](uint32_t jj) { // packet jj's record, j0 < jj <= j0 + 64
                 Rec x;
                 const int l = (int)(jj - j0 - 1u);
@@ -248,11 +256,11 @@ __global__ void __launch_bounds__(64) k_serve(const SrvRec *__restrict__ recs,
             };
             more = false;
             while (r0.seq == seq) {
+                u32x4 d0[kSvLoads], d1[kSvLoads];
+                sv_load(r0.addr, sv_span(r0.len, r0.kind), lane, d0);
                 const bool last_in_batch = j == j0 + 64u; // r1 would need the next batch
                 const Rec r1 = last_in_batch ? Rec{0, 0, 0, 0, ~seq} : rec_at(j + 1u);
                 const bool two = r1.seq == seq;
-                u32x4 d0[kSvLoads], d1[kSvLoads];
-                sv_load(r0.addr, sv_span(r0.len, r0.kind), lane, d0);
                 if (two)
                     sv_load(r1.addr, sv_span(r1.len, r1.kind), lane, d1);
                 auto answer = [&](const Rec &x, const u32x4 (&d)[kSvLoads], uint32_t k) {
