@@ -899,12 +899,15 @@ int serve_batch(Device &D, int dev, const uint8_t *dbase, const uint64_t *h_off,
         seq = 1;
     S.seq = seq;
     const uint32_t rkind = kind == kKindRx ? wc::kSrvKindRx : (uint32_t)kind;
+    if ((uint64_t)dbase + h_off[n - 1] >= (1ull << wc::kSrvAddrBits) ||
+        (uint64_t)dbase >= (1ull << wc::kSrvAddrBits))
+        return kSrvFallback; // the record packs the count above a 48-bit address
     // Last packet first: a wave that sees its first record current finds
     // every later one of the request current too (stores become visible in
     // program order).
     for (uint64_t k = n; k-- > 0;) {
         wc::SrvRec &r = S.h_rec[k];
-        r.addr = (uint64_t)(dbase + h_off[k]);
+        r.addr = (uint64_t)(dbase + h_off[k]) | (n << wc::kSrvAddrBits);
         r.info = (uint32_t)h_len[k] | (rkind << 16);
         __atomic_store_n(&r.seq, seq, __ATOMIC_RELEASE);
     }

@@ -180,8 +180,9 @@ hipError_t launch_rx_verdict(const void *base, const uint64_t *offs, const uint1
 constexpr uint32_t kSrvMaxPkts = 1024;  // packets per request
 constexpr uint32_t kSrvMaxBytes = 4064; // bytes one packet (frame) may span
 constexpr uint32_t kSrvKindRx = 2;      // record kind beside WC_KIND_IP / _PAYLOAD
+constexpr int kSrvAddrBits = 48;        // the packet count rides above the address
 struct alignas(16) SrvRec {
-    uint64_t addr; // device address of the packet / frame
+    uint64_t addr; // device address of the packet / frame (< 2^48) | n << 48
     uint32_t info; // len | kind << 16 | stop << 24
     uint32_t seq;  // request number, stored last
 };

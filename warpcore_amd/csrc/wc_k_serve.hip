@@ -55,8 +55,14 @@ __device__ __forceinline__ u32x4 load_sys16(const void *p)
 
 struct Rec {
     uint64_t addr;
-    uint32_t len, kind, stop, seq;
+    uint32_t len, kind, stop, seq, n; // n: the request's packet count
 };
+
+__device__ __forceinline__ void rec_addr(Rec &x, uint32_t lo, uint32_t hi)
+{
+    x.addr = (uint64_t)lo | ((uint64_t)(hi & ((1u << (kSrvAddrBits - 32)) - 1u)) << 32);
+    x.n = hi >> (kSrvAddrBits - 32);
+}
 
 __device__ __forceinline__ Rec rec_load(const SrvRec *r)
 {
@@ -67,7 +73,7 @@ __device__ __forceinline__ Rec rec_load(const SrvRec *r)
     v.z = (uint32_t)__builtin_amdgcn_readfirstlane((int)v.z);
     v.w = (uint32_t)__builtin_amdgcn_readfirstlane((int)v.w);
     Rec x;
-    x.addr = (uint64_t)v.x | ((uint64_t)v.y << 32);
+    rec_addr(x, v.x, v.y);
     x.len = v.z & 0xFFFFu;
     x.kind = (v.z >> 16) & 0xFFu;
     x.stop = v.z >> 24;
@@ -235,22 +241,28 @@ __global__ void __launch_bounds__(64) k_serve(const SrvRec *__restrict__ recs,
             // (two 8-byte system-scope loads the compiler waits for only at
             // first use: in flight with packet j0's loads; records written
             // before the one already seen need no single-snapshot load)
-            const uint64_t *rp = (const uint64_t *)&recs[kx < kSrvMaxPkts ? kx : w];
-            const uint64_t rlo = __hip_atomic_load(rp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            const uint64_t rhi =
-                __hip_atomic_load(rp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            // Only this wave's packets of the request are read: n (in every
+            // record) gives their count, so a request of n <= W packets reads
+            // no further record at all.
+            const uint32_t nrec = r.n > w ? (r.n - w + W - 1u) / W : 0u;
+            uint64_t rlo = 0, rhi = 0;
+            if (j0 + 1u + (uint32_t)lane < nrec && kx < kSrvMaxPkts) {
+                const uint64_t *rp = (const uint64_t *)&recs[kx];
+                rlo = __hip_atomic_load(rp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                rhi = __hip_atomic_load(rp + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
             const u32x4 rv = {(uint32_t)rlo, (uint32_t)(rlo >> 32), (uint32_t)rhi,
                               (uint32_t)(rhi >> 32)};
             auto rec_at = [&](uint32_t jj) { // packet jj's record, j0 < jj <= j0 + 64
                 Rec x;
                 const int l = (int)(jj - j0 - 1u);
-                x.addr = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)rv.x, l) |
-                         ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)rv.y, l) << 32);
+                rec_addr(x, (uint32_t)__builtin_amdgcn_readlane((int)rv.x, l),
+                         (uint32_t)__builtin_amdgcn_readlane((int)rv.y, l));
                 const uint32_t z = (uint32_t)__builtin_amdgcn_readlane((int)rv.z, l);
                 x.len = z & 0xFFFFu;
                 x.kind = (z >> 16) & 0xFFu;
                 x.stop = z >> 24;
-                x.seq = w + jj * W < kSrvMaxPkts
+                x.seq = jj < nrec && w + jj * W < kSrvMaxPkts
                             ? (uint32_t)__builtin_amdgcn_readlane((int)rv.w, l) : ~seq;
                 return x;
             };
@@ -259,7 +271,7 @@ __global__ void __launch_bounds__(64) k_serve(const SrvRec *__restrict__ recs,
                 u32x4 d0[kSvLoads], d1[kSvLoads];
                 sv_load(r0.addr, sv_span(r0.len, r0.kind), lane, d0);
                 const bool last_in_batch = j == j0 + 64u; // r1 would need the next batch
-                const Rec r1 = last_in_batch ? Rec{0, 0, 0, 0, ~seq} : rec_at(j + 1u);
+                const Rec r1 = last_in_batch ? Rec{0, 0, 0, 0, ~seq, 0} : rec_at(j + 1u);
                 const bool two = r1.seq == seq;
                 if (two)
                     sv_load(r1.addr, sv_span(r1.len, r1.kind), lane, d1);
