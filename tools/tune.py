@@ -246,8 +246,13 @@ def main():
                         print(f"!! variant {name!r} results differ", flush=True)
             else:
                 g, u, nt = cfg
-                fn = lambda: slib.stream_read(buf.data_ptr(), nbytes, g, u, nt,  # noqa: E731
-                                              sink.data_ptr(), stream.cuda_stream)
+                rb = [0]
+                pool = bufs if args.config in ("c2", "c3") else [buf]
+
+                def fn():  # the plain read of the batch, rotating like the checksum
+                    rb[0] = (rb[0] + 1) % len(pool)
+                    slib.stream_read(pool[rb[0]].data_ptr(), nbytes, g, u, nt,
+                                     sink.data_ptr(), stream.cuda_stream)
                 if name.startswith("TILEREAD"):
                     fn = lambda: slib.tile_read(buf.data_ptr(), nbytes, g, u, nt,  # noqa: E731
                                                 sink.data_ptr(), stream.cuda_stream)
