@@ -147,7 +147,10 @@ def main():
         n = args.packets
         stride = args.stride or L
         nbytes = n * L
-        K = max(1, -(-args.rotate_bytes // (args.offset + n * stride))) if args.rotate_bytes else 1
+        # Bytes a batch pulls through the caches: its span when packed, about
+        # one line pair per packet when sparse (bench.py's rotation rule).
+        touched = n * min(stride, L + 128) if stride > L + 128 else args.offset + n * stride
+        K = max(1, -(-args.rotate_bytes // touched)) if args.rotate_bytes else 1
         bufs = []
         for k in range(K):
             b = torch.empty(args.offset + n * stride + 64, dtype=torch.uint8, device=dev)
@@ -222,6 +225,7 @@ def main():
 
     times = {c[0]: [] for c in cases}
     ref = None
+    rot = locals().get("rot") if args.config in ("c2", "c3") and not (args.fused or args.ragged) else None
     for r in range(args.rounds):
         for name, cfg in cases:
             if cfg is None:
@@ -239,6 +243,9 @@ def main():
                     torch.cuda.synchronize()
                 ms = time_it(run, args.iters, stream)
                 if r == 0:
+                    if rot is not None:  # compare every variant on the same buffer
+                        rot[0] = -1
+                        run()
                     res = out.cpu().numpy().copy()
                     if ref is None:
                         ref = res

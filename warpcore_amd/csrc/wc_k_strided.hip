@@ -54,7 +54,14 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
     // slower elsewhere (2048-B slots at +14: 128 B 41.4 -> 37.3 %, 576 B 78 ->
     // 75.6 %, 1024 B on 16 x 5 77.3 -> 69.1 %, 9000 B on 32 x 18 92 -> 26 %:
     // profiles/ab_r03_strided_asip.log).
-    constexpr bool ASIP = KIND == WC_KIND_PAYLOAD && !HDR && G * CPL == 96;
+    // (Tuning build: WC_VARIANT bit 27 turns ASIP on for every shape.)
+    constexpr bool ASIP_CT = KIND == WC_KIND_PAYLOAD && !HDR && G * CPL == 96;
+#ifdef WC_TUNING
+    constexpr bool ASIP_ANY = KIND == WC_KIND_PAYLOAD && !HDR;
+#else
+    constexpr bool ASIP_ANY = ASIP_CT;
+#endif
+    const bool ASIP = ASIP_CT || (ASIP_ANY && (variant & (1 << 27)));
 
     const int lane = threadIdx.x & 63;
     const int gl = lane & (G - 1);
@@ -140,13 +147,13 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
                     b3 = __shfl(pick_byte(d[u][0], (su + 3) & 15), lead + ((su + 3) >> 4), 64);
                     b6 = __shfl(pick_byte(d[u][0], (su + 6) & 15), lead + ((su + 6) >> 4), 64);
                 };
-                if (ASIP || !(variant & (1 << 19))) {
+                if (ASIP_ANY || !(variant & (1 << 19))) {
                     // DPP broadcasts of the window dwords that hold packet
                     // bytes 0..7 (0..11 for ASIP) (window dword k is dword
                     // k & 3 of group lane k >> 2); the ds_bpermute exchange
                     // (WC_VARIANT bit 19) cost 2048-B netmap slots 4 points,
                     // packed 64-192 B 2-5 points (profiles/ab_r02_hdr_dpp.log).
-                    constexpr int NW = ASIP ? 4 : 3;
+                    constexpr int NW = ASIP_ANY ? 4 : 3;
                     uint32_t w[NW];
 #pragma unroll
                     for (int j = 0; j < NW; ++j) {
@@ -160,7 +167,7 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
                     const uint32_t sh = 8u * (uint32_t)(su & 3);
                     const uint32_t x0 = __builtin_amdgcn_alignbit(w[1], w[0], sh); // 0..3
                     x1 = __builtin_amdgcn_alignbit(w[2], w[1], sh);                // 4..7
-                    if constexpr (ASIP)
+                    if constexpr (ASIP_ANY)
                         x2 = __builtin_amdgcn_alignbit(w[3], w[2], sh); // 8..11
                     b0 = x0 & 0xFFu;
                     b2 = (x0 >> 16) & 0xFFu;
@@ -170,7 +177,7 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
                     exchange();
                 }
                 ph = pseudo_hdr(b0, b2, b3, b6);
-                if constexpr (ASIP) {
+                if (ASIP) {
                     ok = ph.v4 ? ph.hl == 20u && plen[u] >= 20u : plen[u] >= 40u;
                     extra = ph.v4 ? ph.special - ((x2 & 0xFFu) + ((x2 >> 16) & 0xFFu) +
                                                   ((x2 >> 24) << 8))
@@ -203,7 +210,7 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
                 }
             };
             uint32_t S;
-            if constexpr (ASIP) {
+            if (ASIP) {
                 sum_packet(std::integral_constant<int, WC_KIND_IP>{}, 8);
                 S = combine(E, O, s[u] & 1) + (gl == 0 ? extra : 0u);
                 if (__ballot(valid[u] && !ok)) { // rare: redo the round with header ranges
