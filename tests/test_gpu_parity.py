@@ -140,6 +140,11 @@ PLANNED = [
     (0, 256, 256, "ip", (8, 2, 2)),           # lean kernel, the pass filled exactly
     (0, 576, 576, "ip", (16, 3, 1)),
     (0, 9000, 9000, "ip", (32, 18, 1)),
+    (14, 2048, 64, "ip", (8, 1, 4)),          # small packets in netmap slots
+    (14, 2048, 64, "payload", (4, 2, 2)),
+    (14, 2048, 128, "ip", (8, 3, 2)),
+    (14, 2048, 128, "payload", (4, 2, 2)),    # sparse payload, 7..16 chunks
+    (14, 2048, 240, "payload", (4, 2, 2)),
 ]
 
 

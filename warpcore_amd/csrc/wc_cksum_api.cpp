@@ -331,16 +331,18 @@ wc::Shape shape_for_chunks(uint32_t nch, bool full, bool payload, bool aligned,
     // run at the rate of the cache lines they touch, one or two per packet;
     // shapes with more lanes per packet reach it (2048-B slots at +14,
     // profiles/ab_r03_slot_shapes.log): ip_cksum 5-6 chunks on 8 x 1 x 4
-    // (64 / 72 / 80 B: 36 -> 41, 41 -> 47, 46 -> 52 %), payload_cksum 9-16
-    // chunks on 8 x 2 x 4 (128 / 160 / 200 / 240 B: 37 -> 40, 46 -> 51,
-    // 57 -> 62, 69 -> 76 %).  payload_cksum keeps 4 x 2 x 2 at 5-6 chunks
-    // (8 x 1 x 4: 36 -> 28 %).
-    if (nch <= 6)
+    // (64 / 72 / 80 B: 36 -> 41, 41 -> 47, 46 -> 52 %).  payload_cksum keeps
+    // 4 x 2 x 2 there (8 x 1 x 4: 36 -> 28 %: its header hand-off between
+    // lanes costs more the wider the group), and takes it for sparse packets
+    // of up to 16 chunks too, even where that is two passes: read from HBM
+    // (rotating buffers, round 4) it beats the (8,1,4) / (8,2,4) round 3
+    // picked on Infinity-Cache-resident reruns -- 96 B 35.6 -> 27.2 us, 128 B
+    // 49.2 -> 44.4, 160 B 49.6 -> 44.3, 200 B 50.0 -> 46.2, 240 B 48.4 ->
+    // 45.9 (profiles/ab_r04_payload_small.log).
+    if (nch <= 6 || (sparse && payload && nch <= 16))
         return sparse && !payload ? wc::Shape{8, 1, 4} : wc::Shape{4, 2, 2};
     if (nch <= 8)
         return {8, 1, 4};
-    if (sparse && payload && nch <= 16)
-        return {8, 2, 4};
     // 9..24 chunks: 8 lanes x 3 chunks, two packets per group -- fewer dead
     // lane slots than 16 x 2 (profiles/sweep_r01_mid_shapes.log: 256 B 78.7 -> 84.1 %,
     // 200 B 55 -> 67.5 %, 256 B at +14 50 -> 60 % of HBM peak)
