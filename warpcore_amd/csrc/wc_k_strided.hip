@@ -6,6 +6,18 @@
 
 namespace wc {
 
+// payload_cksum's header window dwords K0 .. K0 + NW - 1 of a packet whose
+// start phase in its 16-byte chunk is the same for the whole batch (stride a
+// multiple of 16): window dword k is dword k & 3 of group lane k >> 2, both
+// known at compile time here, so each word is one broadcast from one lane and
+// no per-lane select.
+template <int G, int K0, int... J>
+__device__ __forceinline__ void hdr_words_uni(const u32x4 &d0, uint32_t *w,
+                                              std::integer_sequence<int, J...>)
+{
+    ((w[J] = group_bcast<G, ((K0 + J) >> 2)>(d0[(K0 + J) & 3])), ...);
+}
+
 // ---------------------------------------------------------------------------
 // Strided batches: group-per-packet kernel.
 //   G     lanes per packet (power of two, 4..64)
@@ -147,7 +159,35 @@ k_cksum(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len,
                     b3 = __shfl(pick_byte(d[u][0], (su + 3) & 15), lead + ((su + 3) >> 4), 64);
                     b6 = __shfl(pick_byte(d[u][0], (su + 6) & 15), lead + ((su + 6) >> 4), 64);
                 };
-                if (ASIP_ANY || !(variant & (1 << 19))) {
+                if (variant & (1 << 29)) { // timing probe (tuning build): no hand-off, wrong results
+                    b0 = 0x45u;
+                    b2 = 0u;
+                    b3 = 64u;
+                    b6 = 17u;
+                } else if (!RAGGED && (stride & 15u) == 0 && !(variant & (1 << 30))) {
+                    // One start phase for the batch: the window dwords and
+                    // their lanes are wave-uniform (tuning build: WC_VARIANT
+                    // bit 30 takes the per-lane path below instead).
+                    constexpr int NW = ASIP_ANY ? 4 : 3;
+                    uint32_t w[NW];
+                    const int su0 = __builtin_amdgcn_readfirstlane(su);
+                    using Seq = std::make_integer_sequence<int, NW>;
+                    switch (su0 >> 2) {
+                    case 0: hdr_words_uni<G, 0>(d[u][0], w, Seq{}); break;
+                    case 1: hdr_words_uni<G, 1>(d[u][0], w, Seq{}); break;
+                    case 2: hdr_words_uni<G, 2>(d[u][0], w, Seq{}); break;
+                    default: hdr_words_uni<G, 3>(d[u][0], w, Seq{}); break;
+                    }
+                    const uint32_t sh = 8u * (uint32_t)(su0 & 3);
+                    const uint32_t x0 = __builtin_amdgcn_alignbit(w[1], w[0], sh); // 0..3
+                    x1 = __builtin_amdgcn_alignbit(w[2], w[1], sh);                // 4..7
+                    if constexpr (ASIP_ANY)
+                        x2 = __builtin_amdgcn_alignbit(w[3], w[2], sh); // 8..11
+                    b0 = x0 & 0xFFu;
+                    b2 = (x0 >> 16) & 0xFFu;
+                    b3 = x0 >> 24;
+                    b6 = (x1 >> 16) & 0xFFu;
+                } else if (ASIP_ANY || !(variant & (1 << 19))) {
                     // DPP broadcasts of the window dwords that hold packet
                     // bytes 0..7 (0..11 for ASIP) (window dword k is dword
                     // k & 3 of group lane k >> 2); the ds_bpermute exchange
