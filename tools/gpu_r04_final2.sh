@@ -20,5 +20,5 @@ print('value', d['value'], 'frac', r['frac'], 'frac_rotating', r.get('frac_rotat
 print('c3', {k: v.get('frac') for k, v in d.get('c3', {}).get('sizes', {}).items()})
 print('c4', d.get('c4', {}).get('frac') if isinstance(d.get('c4'), dict) else d.get('c4'))
 "
-CFGS="s14pl_64 s14pl_128 s14pl_256 s14_64 s14_128" TAG=r04c bash tools/round_measure.sh \
+CFGS="${CFGS:-s14pl_64 s14pl_128 s14pl_256 s14_64 s14_128}" TAG=${TAG:-r04c} bash tools/round_measure.sh \
     > gpurun_out/round_r04c.log 2>&1
