@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# Round 4 closing GPU call: the full GPU test suite, smoke(), the default
+# Closing GPU call of a round: the full GPU test suite, smoke(), the default
 # bench line (as the driver runs it), then bench + rocprof for small
 # payload_cksum packets in 2048-B slots after the planner change.
 set -u
