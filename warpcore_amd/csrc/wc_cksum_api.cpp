@@ -882,6 +882,11 @@ int serve_batch(Device &D, int dev, const uint8_t *dbase, const uint64_t *h_off,
     Server &S = D.srv;
     if (S.broken)
         return kSrvFallback;
+    // The record packs the count above a 48-bit address: every packet's
+    // (offsets come in any order).
+    for (uint64_t k = 0; k < n; ++k)
+        if ((uint64_t)dbase + h_off[k] >= (1ull << wc::kSrvAddrBits))
+            return kSrvFallback;
     int rc = server_init_locked(S);
     if (rc)
         return rc;
@@ -901,9 +906,6 @@ int serve_batch(Device &D, int dev, const uint8_t *dbase, const uint64_t *h_off,
         seq = 1;
     S.seq = seq;
     const uint32_t rkind = kind == kKindRx ? wc::kSrvKindRx : (uint32_t)kind;
-    if ((uint64_t)dbase + h_off[n - 1] >= (1ull << wc::kSrvAddrBits) ||
-        (uint64_t)dbase >= (1ull << wc::kSrvAddrBits))
-        return kSrvFallback; // the record packs the count above a 48-bit address
     // Last packet first: a wave that sees its first record current finds
     // every later one of the request current too (stores become visible in
     // program order).
