@@ -75,3 +75,31 @@ def test_build_staleness_is_a_source_hash():
     assert _build.lib_is_current()
     stamp = _build._stamp(_build.LIB)
     assert stamp.read_text().strip() == _build._src_hash(_build.HIP_DEPS, _build.lib_flags())
+
+
+def test_argument_errors_need_no_gpu():
+    """The C ABI rejects bad arguments before it touches a device, the way
+    the reference's callers see errors: WC_EINVAL for a NULL buffer or result
+    pointer and an unknown kind, WC_OK for an empty batch -- none of these
+    calls reaches HIP, so they run here without a GPU."""
+    lib = _lib.load()
+    ok, einval = 0, -10001
+    p = 0x100000  # never dereferenced: every call below returns first
+    # empty batches
+    assert lib.wc_cksum_strided(None, 2048, 64, 0, None, 0, None) == ok
+    assert lib.wc_cksum_ragged(None, None, None, 0, None, 1, None) == ok
+    assert lib.wc_rx_verdict_ragged(None, None, None, 0, None, None, None) == ok
+    # missing result arrays
+    assert lib.wc_cksum_strided(p, 2048, 64, 8, None, 0, None) == einval
+    assert lib.wc_cksum_ragged(p, p, p, 8, None, 0, None) == einval
+    assert lib.wc_verify_strided(p, 2048, 64, 8, p, None, 0, None) == einval
+    assert lib.wc_cksum_ip_udp_strided(p, 2048, 64, 8, None, p, None) == einval
+    assert lib.wc_cksum_ip_udp_strided(p, 2048, 64, 8, p, None, None) == einval
+    # missing packet arrays
+    assert lib.wc_cksum_strided(None, 2048, 64, 8, p, 0, None) == einval
+    assert lib.wc_cksum_ragged(p, None, p, 8, p, 0, None) == einval
+    assert lib.wc_rx_verdict_ragged(p, p, None, 8, p, None, None) == einval
+    # unknown kind (WC_CKSUM_IP = 0, WC_CKSUM_PAYLOAD = 1)
+    assert lib.wc_cksum_strided(p, 2048, 64, 8, p, 7, None) == einval
+    assert lib.wc_cksum_ragged(p, p, p, 8, p, -1, None) == einval
+    assert lib.wc_strerror(einval).decode() == "invalid argument"
