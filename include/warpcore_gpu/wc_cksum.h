@@ -145,6 +145,28 @@ int wc_rx_verdict_host(const void *h_base, uint64_t h_bytes, const uint64_t *h_o
 int wc_cksum_host(const void *h_base, uint64_t h_bytes, const uint64_t *h_off,
                   const uint16_t *h_len, uint64_t n, uint16_t *h_out, int kind);
 
+/* The fused TX pair over host-memory IP packets (each at its IP header, len =
+ * IP header + UDP length, as udp_tx hands them to payload_cksum):
+ * h_out_payload[i] = payload_cksum(pkt, len) and h_out_ip_hdr[i] =
+ * ip_cksum(pkt, ip4_hl(pkt[0])) for IPv4 (0 for IPv6) -- the two checksums
+ * mk_ip4_hdr and udp_tx compute per iov inside w_tx's loop (ip4.c:184-186,
+ * udp.c:209-213, backend_netmap.c:348-358), for a whole w_iov_sq in one
+ * call, one read of each packet's bytes.  Both fields must hold 0 in the
+ * bytes (as the reference zeroes them before summing); store each result
+ * raw.  Same paths and rules as wc_cksum_host: a small registered batch is
+ * answered by the resident server or one zero-copy launch, anything else is
+ * pipelined.  An IPv4 header (hl bytes, options included) must lie inside
+ * [h_base, h_base + h_bytes) even where len is shorter.  Synchronous. */
+int wc_cksum_ip_udp_host(const void *h_base, uint64_t h_bytes, const uint64_t *h_off,
+                         const uint16_t *h_len, uint64_t n, uint16_t *h_out_ip_hdr,
+                         uint16_t *h_out_payload);
+
+/* The resident small-batch server's counters since the process started, over
+ * every device (any pointer may be NULL): batches it answered, batches it was
+ * asked for but could not answer (they took the launch path instead), and
+ * grid launches. */
+int wc_server_stats(uint64_t *served, uint64_t *fallbacks, uint64_t *launches);
+
 /* Page-lock a host region (e.g. the netmap buffer area w->mem,
  * backend_netmap.c:149-151) so wc_cksum_host can DMA from it directly.
  * Registering the same base again drops the old registration and pins the

@@ -769,6 +769,93 @@ def test_host_zero_copy_small_batches(gpu, kind, n):
     np.testing.assert_array_equal(got, want)
 
 
+def fused_want(pool, offs, lens):
+    """The fused TX pair by the oracle: ip_cksum(pkt, hl) of each IPv4 packet
+    (0 for IPv6) and payload_cksum(pkt, len) (ip4.c:184-186, udp.c:209-213)."""
+    b0 = pool[offs.astype(np.int64)]
+    v4 = (b0 >> 4) == 4
+    hl = np.where(v4, (b0 & 0x0F).astype(np.uint16) * 4, 0).astype(np.uint16)
+    hdr = np.where(v4, c_oracle.cksum_ragged(pool, offs, hl, kind=0), 0).astype(np.uint16)
+    return hdr, c_oracle.cksum_ragged(pool, offs, lens, kind=1)
+
+
+@pytest.mark.parametrize("n,register", [(1, True), (64, True), (256, True), (1000, True),
+                                        (6000, True), (64, False), (3000, False)])
+def test_host_fused_ip_udp(gpu, n, register):
+    """wc_cksum_ip_udp_host: the IPv4 header checksum and payload_cksum of
+    host-memory packets in one call -- the resident server (registered, <=
+    256 packets), one zero-copy launch (registered, <= 4096), the pipeline
+    (larger, or pageable), slots in scrambled order.  Wild headers: IPv4
+    options (IHL up to 15), IHL < 5, bad total lengths, IPv6 with any next
+    header.  (len >= hl always: payload_cksum of len < hl reads ~4 GiB in
+    the reference, in_cksum.c:164.)"""
+    rng = np.random.default_rng(n * 3 + register)
+    slot = 2048
+    nslots = max(n, 64)
+    pool = rng.integers(0, 256, nslots * slot + 64, dtype=np.uint8)
+    pkts = random_packets(rng, n, max_payload=slot - 100, wild=True)
+    slots = rng.permutation(nslots)[:n]
+    offs = (slots * slot + rng.integers(0, 16, n)).astype(np.uint64)
+    lens = np.array([ln for _, ln in pkts], dtype=np.uint16)
+    for o, (p, _) in zip(offs, pkts):
+        pool[int(o): int(o) + len(p)] = np.frombuffer(p, dtype=np.uint8)
+    want_h, want_p = fused_want(pool, offs, lens)
+    if register:
+        wc.host_register(pool)
+    s0 = wc.server_stats()
+    try:
+        got_h, got_p = wc.cksum_ip_udp_host(pool, offs, lens)
+    finally:
+        if register:
+            wc.host_unregister(pool)
+    s1 = wc.server_stats()
+    np.testing.assert_array_equal(got_h, want_h)
+    np.testing.assert_array_equal(got_p, want_p)
+    served = 1 if register and n <= 256 else 0
+    assert (s1["served"] - s0["served"], s1["fallbacks"] - s0["fallbacks"]) == (served, 0)
+
+
+def test_host_fused_round_trip(gpu):
+    """TX -> RX through the host path: both results of wc_cksum_ip_udp_host
+    stored raw into headers whose fields were 0 (mk_ip4_hdr, udp_tx), then
+    ip_cksum over the header and payload_cksum over the packet give 0 (the RX
+    checks, ip4.c:110-115 and udp.c:134) -- and the RX verdict of every frame
+    is WC_RX_OK."""
+    rng = np.random.default_rng(99)
+    n, slot = 200, 2048
+    frames = []
+    for i in range(n):
+        payload = rng.integers(0, 256, int(rng.integers(0, 1400)), dtype=np.uint8).tobytes()
+        pkt, ln = (ipv6_udp(payload, rng) if i % 3 == 0 else
+                   ipv4_udp(payload, rng, ihl=5 if i % 5 else 7))
+        frames.append((pkt, ln))
+    pool = np.zeros(n * slot, dtype=np.uint8)
+    offs = (np.arange(n) * slot + 14).astype(np.uint64)  # IP header at +14 in a slot
+    lens = np.array([ln for _, ln in frames], dtype=np.uint16)
+    for o, (p, _) in zip(offs, frames):
+        pool[int(o) - 2: int(o)] = [0x86, 0xDD] if p[0] >> 4 == 6 else [0x08, 0x00]
+        pool[int(o): int(o) + len(p)] = np.frombuffer(p, dtype=np.uint8)
+    wc.host_register(pool)
+    try:
+        hdr, pay = wc.cksum_ip_udp_host(pool, offs, lens)
+        for i, o in enumerate(offs.astype(np.int64)):
+            v4 = pool[o] >> 4 == 4
+            hl = (pool[o] & 0x0F) * 4 if v4 else 40
+            if v4:
+                pool[o + 10: o + 12] = np.frombuffer(np.uint16(hdr[i]).tobytes(), np.uint8)
+            pool[o + hl + 6: o + hl + 8] = np.frombuffer(np.uint16(pay[i]).tobytes(), np.uint8)
+        v4 = (pool[offs.astype(np.int64)] >> 4) == 4
+        hl = np.where(v4, (pool[offs.astype(np.int64)] & 0x0F).astype(np.uint16) * 4, 0)
+        assert (wc.cksum_host(pool, offs[v4], hl[v4].astype(np.uint16), kind="ip") == 0).all()
+        assert (wc.cksum_host(pool, offs, lens, kind="payload") == 0).all()
+        verdict, drops = wc.rx_verdict_host(pool, offs - 14, lens + 14)
+    finally:
+        wc.host_unregister(pool)
+    assert drops == 0
+    ok = (verdict == wc.RX_OK) | ((verdict == wc.RX_OK_NO_CKSUM) & (pay == 0))
+    assert ok.all(), verdict
+
+
 @pytest.mark.parametrize("waves", ["64", "7"])
 def test_host_resident_server(gpu, monkeypatch, waves):
     """Small registered batches answered by the resident server (wc_k_serve:
@@ -784,6 +871,7 @@ def test_host_resident_server(gpu, monkeypatch, waves):
     slot = 8192
     pool = rng.integers(0, 256, 512 * slot, dtype=np.uint8)
     wc.host_register(pool)
+    s0 = wc.server_stats()
     try:
         for n in (1, 2, 7, 64, 65, 300, 1024):
             for kind in ("ip", "payload"):
@@ -809,10 +897,65 @@ def test_host_resident_server(gpu, monkeypatch, waves):
         lens = np.full(64, 1472, dtype=np.uint16)
         np.testing.assert_array_equal(wc.cksum_host(pool, offs, lens),
                                       c_oracle.cksum_ragged(pool, offs, lens))
+        s1 = wc.server_stats()
+        # every batch but n = 7 (a packet past 4064 B: the launch path) was
+        # answered by the server, none fell back; idle stop + restart = a
+        # second grid launch at least
+        assert s1["served"] - s0["served"] == 13, (s0, s1)
+        assert s1["fallbacks"] == s0["fallbacks"], (s0, s1)
+        assert s1["launches"] - s0["launches"] >= 2, (s0, s1)
     finally:
         wc.host_unregister(pool)
         monkeypatch.delenv("WC_SERVE_WAVES")
         monkeypatch.delenv("WC_SERVE_MAX")
+        wc.reload_config()
+
+
+def test_host_server_light_traffic_then_full_batch(gpu, monkeypatch):
+    """under steady light traffic (1-packet calls, every
+    other wave never sees a request) past the grid's own 4-s drain time, a
+    batch that needs every wave is still answered by the server -- no wave
+    left on its own clock (the heartbeat keeps the grid whole), no fallback,
+    no relaunch.  Then a grid left idle past half its drain time (the idle
+    watcher held off) is restarted by the next call, not half-used."""
+    import time
+    monkeypatch.setenv("WC_SERVE_WAVES", "64")
+    monkeypatch.setenv("WC_SERVE_IDLE_US", "30000000")  # the watcher stays out of it
+    wc.reload_config()
+    rng = np.random.default_rng(77)
+    slot = 2048
+    pool = rng.integers(0, 256, 256 * slot, dtype=np.uint8)
+    wc.host_register(pool)
+    try:
+        one_off = np.array([3], dtype=np.uint64)
+        one_len = np.array([1472], dtype=np.uint16)
+        want1 = c_oracle.cksum_ragged(pool, one_off, one_len)
+        wc.cksum_host(pool, one_off, one_len)  # starts the grid
+        s0 = wc.server_stats()
+        t0 = time.monotonic()
+        calls = 0
+        while time.monotonic() - t0 < 4.6:  # past kSrvSafetyMs (4 s)
+            np.testing.assert_array_equal(wc.cksum_host(pool, one_off, one_len), want1)
+            calls += 1
+            time.sleep(0.002)
+        offs = (np.arange(200, dtype=np.uint64) * slot + 7).astype(np.uint64)
+        lens = rng.integers(0, 2000, 200).astype(np.uint16)
+        want = c_oracle.cksum_ragged(pool, offs, lens)
+        t1 = time.monotonic()
+        np.testing.assert_array_equal(wc.cksum_host(pool, offs, lens), want)
+        assert time.monotonic() - t1 < 0.5  # answered at once, no 50-ms / 2-s wait
+        s1 = wc.server_stats()
+        assert s1["served"] - s0["served"] == calls + 1, (s0, s1)
+        assert (s1["fallbacks"], s1["launches"]) == (s0["fallbacks"], s0["launches"]), (s0, s1)
+        time.sleep(2.3)  # idle past half the drain time: the next call restarts it
+        np.testing.assert_array_equal(wc.cksum_host(pool, offs, lens), want)
+        s2 = wc.server_stats()
+        assert s2["served"] - s1["served"] == 1 and s2["fallbacks"] == s1["fallbacks"], (s1, s2)
+        assert s2["launches"] - s1["launches"] == 1, (s1, s2)
+    finally:
+        wc.host_unregister(pool)
+        monkeypatch.delenv("WC_SERVE_WAVES")
+        monkeypatch.delenv("WC_SERVE_IDLE_US")
         wc.reload_config()
 
 

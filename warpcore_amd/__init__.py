@@ -6,6 +6,7 @@ This package is the Python host mirror of that C ABI plus the synthetic
 packet generators and the multi-GPU shard driver used by bench.py.
 """
 from .cksum import (KIND_IP, KIND_PAYLOAD, WcError, cksum_host, cksum_host_multi,
+                    cksum_ip_udp_host, server_stats,
                     cksum_ip_udp_ragged, cksum_ragged_multi, gather_results_multi,
                     gpu_init_multi, shard_range,
                     cksum_ip_udp_strided, cksum_ragged, cksum_strided, gpu_init, host_register, host_unregister,
@@ -17,6 +18,7 @@ from .cksum import (KIND_IP, KIND_PAYLOAD, WcError, cksum_host, cksum_host_multi
 
 __all__ = [
     "KIND_IP", "KIND_PAYLOAD", "WcError", "cksum_host", "cksum_host_multi",
+    "cksum_ip_udp_host", "server_stats",
     "cksum_ip_udp_ragged", "cksum_ragged_multi", "gather_results_multi", "gpu_init_multi",
     "shard_range",
     "cksum_ip_udp_strided", "cksum_ragged",

@@ -35,6 +35,9 @@ SIGNATURES = {
     "wc_rx_verdict_ragged": (_int, [_vp, _vp, _vp, _u64, _vp, _vp, _vp]),
     "wc_rx_verdict_host": (_int, [_vp, _u64, _vp, _vp, _u64, _vp, _vp]),
     "wc_cksum_host": (_int, [_vp, _u64, _vp, _vp, _u64, _vp, _int]),
+    "wc_cksum_ip_udp_host": (_int, [_vp, _u64, _vp, _vp, _u64, _vp, _vp]),
+    "wc_server_stats": (_int, [ctypes.POINTER(_u64), ctypes.POINTER(_u64),
+                               ctypes.POINTER(_u64)]),
     "wc_host_register": (_int, [_vp, _u64]),
     "wc_host_unregister": (_int, [_vp]),
     "wc_gpu_init": (_int, [_int]),

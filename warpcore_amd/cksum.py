@@ -392,6 +392,43 @@ def cksum_host(buf: np.ndarray, offsets: np.ndarray, lengths: np.ndarray,
     return out
 
 
+def _host_batch_args(buf, offsets, lengths):
+    buf = np.ascontiguousarray(buf).reshape(-1).view(np.uint8)
+    lens_in = np.asarray(lengths)
+    if lens_in.size and (lens_in.min() < 0 or lens_in.max() > 0xFFFF):
+        raise ValueError("len is a uint16 in the reference (0..65535)")
+    offs_in = np.asarray(offsets)
+    if offs_in.size and offs_in.dtype.kind == "i" and offs_in.min() < 0:
+        raise ValueError("negative offset")
+    if offs_in.shape != lens_in.shape:
+        raise ValueError("offsets and lengths must have the same shape")
+    return (buf, np.ascontiguousarray(offs_in, dtype=np.uint64),
+            np.ascontiguousarray(lens_in, dtype=np.uint16))
+
+
+def cksum_ip_udp_host(buf: np.ndarray, offsets: np.ndarray,
+                      lengths: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+    """The fused TX pair over host-memory IP packets (wc_cksum_ip_udp_host,
+    synchronous): (IPv4 header checksums -- 0 for IPv6 --, payload_cksum
+    results), what mk_ip4_hdr and udp_tx store (ip4.c:184-186,
+    udp.c:209-213)."""
+    buf, off, lens = _host_batch_args(buf, offsets, lengths)
+    hdr = np.empty(off.size, dtype=np.uint16)
+    out = np.empty(off.size, dtype=np.uint16)
+    _check("wc_cksum_ip_udp_host", _lib.load().wc_cksum_ip_udp_host(
+        buf.ctypes.data, buf.size, off.ctypes.data, lens.ctypes.data, off.size,
+        hdr.ctypes.data, out.ctypes.data))
+    return hdr, out
+
+
+def server_stats() -> dict:
+    """The resident server's counters (wc_server_stats): batches served,
+    fallbacks to the launch path, grid launches -- process totals."""
+    v = [ctypes.c_uint64() for _ in range(3)]
+    _check("wc_server_stats", _lib.load().wc_server_stats(*[ctypes.byref(x) for x in v]))
+    return dict(zip(("served", "fallbacks", "launches"), (x.value for x in v)))
+
+
 # Buffers page-locked through host_register, by base address: the library
 # pins the pages mapped at that address, so the array is kept alive here until
 # host_unregister (a buffer garbage-collected while registered could give its

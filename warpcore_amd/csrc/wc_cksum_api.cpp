@@ -38,9 +38,12 @@ constexpr uint64_t kChunkPkts = 1ull << 20;       // host-path packets per chunk
 constexpr uint64_t kScalarStage = 65536 + 64;     // one max-size packet
 constexpr uint64_t kZcPkts = 4096;                // zero-copy path: max packets
 constexpr int kFlatMinDefault = 0;                // ragged: flat kernel from n >= this
-// Internal batch kind of the host paths beside WC_CKSUM_IP / WC_CKSUM_PAYLOAD:
-// RX verdicts of Ethernet frames (lengths = frame lengths, 1-byte results).
+// Internal batch kinds of the host paths beside WC_CKSUM_IP / WC_CKSUM_PAYLOAD:
+// RX verdicts of Ethernet frames (lengths = frame lengths, 1-byte results),
+// and the fused TX pair (payload_cksum into the main results, the IPv4
+// header's ip_cksum into a second array; wc_cksum_ip_udp_host).
 constexpr int kKindRx = 2;
+constexpr int kKindFused = 3;
 
 // Small batches over registered memory skip the copy engines: the kernel
 // reads the packets straight out of the page-locked region over PCIe, and
@@ -59,10 +62,12 @@ struct HostPipe {
     uint64_t *d_off[kPipe] = {};
     uint16_t *d_len[kPipe] = {};
     uint16_t *d_out[kPipe] = {};
+    uint16_t *d_out2[kPipe] = {};  // fused pass: the IPv4 header checksums
     uint8_t *h_bytes[kPipe] = {};  // pinned staging for unregistered input
     uint64_t *h_off[kPipe] = {};   // pinned, rebased offsets
     uint16_t *h_len[kPipe] = {};
     uint16_t *h_out[kPipe] = {};
+    uint16_t *h_out2[kPipe] = {};
     bool ready = false;
 };
 
@@ -71,6 +76,7 @@ struct ZeroCopy {
     uint64_t *h_off = nullptr, *d_off = nullptr; // mapped pinned
     uint16_t *h_len = nullptr, *d_len = nullptr;
     uint16_t *h_out = nullptr, *d_out = nullptr;
+    uint16_t *h_out2 = nullptr, *d_out2 = nullptr; // fused pass: header checksums
     bool ready = false;
 };
 
@@ -81,11 +87,21 @@ struct Server {
     hipStream_t st = nullptr;
     wc::SrvRec *h_rec = nullptr, *d_rec = nullptr;
     wc::SrvRes *h_res = nullptr, *d_res = nullptr;
+    uint32_t *h_hb = nullptr, *d_hb = nullptr; // heartbeat: the latest request number
     uint32_t seq = 0;
     int waves = 0;
     bool ready = false, running = false, broken = false;
-    std::chrono::steady_clock::time_point last{};
+    // last: the last answered call (the idle watcher's clock); posted: the
+    // grid's launch or its last request (the drain-safety clock)
+    std::chrono::steady_clock::time_point last{}, posted{};
 };
+
+// wc_server_stats, over every device and the whole process (under g_mu):
+// batches the grid answered, batches it was asked for but could not answer
+// (the launch path took them), grid launches.
+struct ServerStats {
+    uint64_t served = 0, fallbacks = 0, launches = 0;
+} g_srv_stats;
 
 struct Device {
     bool ok = false;
@@ -151,8 +167,11 @@ struct Config {
     int rx_skip = 0;               // WC_RX_SKIP: frames the parse rules out leave the stream
     int rx_mode() const
     {
+        // EARLY streams only the frames that need the check already, so
+        // SKIP has nothing to take out: it is dropped rather than sending
+        // EARLY | SKIP to a variant that ignores the HDRT / NT settings.
         return (rx_early ? wc::kRxEarly : 0) | (rx_hdrt ? wc::kRxHdrT : 0) |
-               (rx_skip ? wc::kRxSkip : 0);
+               (rx_skip && !rx_early ? wc::kRxSkip : 0);
     }
 };
 
@@ -662,10 +681,12 @@ void pipe_free(HostPipe &P)
         (void)hipFree(P.d_off[s]);
         (void)hipFree(P.d_len[s]);
         (void)hipFree(P.d_out[s]);
+        (void)hipFree(P.d_out2[s]);
         (void)hipHostFree(P.h_bytes[s]);
         (void)hipHostFree(P.h_off[s]);
         (void)hipHostFree(P.h_len[s]);
         (void)hipHostFree(P.h_out[s]);
+        (void)hipHostFree(P.h_out2[s]);
         if (P.done[s])
             (void)hipEventDestroy(P.done[s]);
         if (P.st[s])
@@ -687,10 +708,12 @@ int pipe_init_locked(HostPipe &P)
             hipMalloc((void **)&P.d_off[s], kChunkPkts * 8) != hipSuccess ||
             hipMalloc((void **)&P.d_len[s], kChunkPkts * 2) != hipSuccess ||
             hipMalloc((void **)&P.d_out[s], kChunkPkts * 2) != hipSuccess ||
+            hipMalloc((void **)&P.d_out2[s], kChunkPkts * 2) != hipSuccess ||
             hipHostMalloc((void **)&P.h_bytes[s], kChunkBytes + 64, 0) != hipSuccess ||
             hipHostMalloc((void **)&P.h_off[s], kChunkPkts * 8, 0) != hipSuccess ||
             hipHostMalloc((void **)&P.h_len[s], kChunkPkts * 2, 0) != hipSuccess ||
-            hipHostMalloc((void **)&P.h_out[s], kChunkPkts * 2, 0) != hipSuccess) {
+            hipHostMalloc((void **)&P.h_out[s], kChunkPkts * 2, 0) != hipSuccess ||
+            hipHostMalloc((void **)&P.h_out2[s], kChunkPkts * 2, 0) != hipSuccess) {
             pipe_free(P);
             return WC_ENOMEM;
         }
@@ -709,9 +732,11 @@ int zc_init_locked(Device &D)
         hipHostMalloc((void **)&Z.h_off, kZcPkts * 8, fl) != hipSuccess ||
         hipHostMalloc((void **)&Z.h_len, kZcPkts * 2, fl) != hipSuccess ||
         hipHostMalloc((void **)&Z.h_out, kZcPkts * 2, fl) != hipSuccess ||
+        hipHostMalloc((void **)&Z.h_out2, kZcPkts * 2, fl) != hipSuccess ||
         hipHostGetDevicePointer((void **)&Z.d_off, Z.h_off, 0) != hipSuccess ||
         hipHostGetDevicePointer((void **)&Z.d_len, Z.h_len, 0) != hipSuccess ||
-        hipHostGetDevicePointer((void **)&Z.d_out, Z.h_out, 0) != hipSuccess)
+        hipHostGetDevicePointer((void **)&Z.d_out, Z.h_out, 0) != hipSuccess ||
+        hipHostGetDevicePointer((void **)&Z.d_out2, Z.h_out2, 0) != hipSuccess)
         return WC_ENOMEM;
     Z.ready = true;
     return WC_OK;
@@ -748,25 +773,39 @@ const uint8_t *registered_dptr_locked(const void *p, uint64_t bytes)
 // header fields up to byte 19 whatever len is, in_cksum.c:149-151).
 uint64_t span_of(uint16_t len, int kind)
 {
-    return kind == WC_CKSUM_PAYLOAD ? std::max<uint64_t>(len, 20) : len;
+    return kind == WC_CKSUM_PAYLOAD || kind == kKindFused ? std::max<uint64_t>(len, 20) : len;
 }
 
-// Result bytes per packet: a uint16 checksum, or a uint8 RX verdict.
+// Bytes the fused TX pair reads of the packet at p (whose first
+// span_of(len, kKindFused) bytes are known to be readable): payload_cksum's,
+// and the IPv4 header's hl bytes ip_cksum sums (ip4.c:184-186) when they run
+// past them (options behind a short len).
+uint64_t fused_span(const uint8_t *p, uint16_t len)
+{
+    const uint64_t s = span_of(len, kKindFused);
+    return (p[0] >> 4) == 4 ? std::max<uint64_t>(s, (uint64_t)(p[0] & 15u) * 4u) : s;
+}
+
+// Result bytes per packet in the main result array: a uint16 checksum, or a
+// uint8 RX verdict.
 int out_size(int kind) { return kind == kKindRx ? 1 : 2; }
 
-// One device launch over a ragged batch of `kind` (a checksum kind or RX
-// verdicts; lengths are frame lengths for the latter).
+// One device launch over a ragged batch of `kind` (a checksum kind, RX
+// verdicts -- lengths are frame lengths --, or the fused pair, whose header
+// checksums go to d_out_hdr).
 int run_ragged_any(const Device &D, const Config &C, const uint8_t *d_base, const uint64_t *d_off,
                    const uint16_t *d_len, uint64_t n, void *d_out, int kind, bool zero_copy,
-                   hipStream_t st)
+                   hipStream_t st, uint16_t *d_out_hdr = nullptr)
 {
     if (kind == kKindRx)
         return hip_err(wc::launch_rx_verdict(d_base, d_off, d_len, n, (uint8_t *)d_out, nullptr,
                                              C.nt != 0, st, C.rx_mode()));
-    const Plan p = plan_ragged(D, C, n, kind, zero_copy);
+    const bool fused = kind == kKindFused;
+    const int k = fused ? WC_CKSUM_PAYLOAD : kind;
+    const Plan p = plan_ragged(D, C, n, k, zero_copy, fused);
     wc::LaunchArgs a{d_base, 0,       0,    d_off, d_len, n,
-                     (uint16_t *)d_out, nullptr, kind, true,  false, C.nt != 0,
-                     C.flat_tpw};
+                     (uint16_t *)d_out, nullptr, k, true,  false, C.nt != 0,
+                     C.flat_tpw, fused ? d_out_hdr : nullptr};
     return run(D, C, a, p, st);
 }
 
@@ -796,33 +835,37 @@ int server_init_locked(Server &S)
     if (hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking) != hipSuccess ||
         hipHostMalloc((void **)&S.h_rec, wc::kSrvMaxPkts * sizeof(wc::SrvRec), fl) != hipSuccess ||
         hipHostMalloc((void **)&S.h_res, wc::kSrvMaxPkts * sizeof(wc::SrvRes), fl) != hipSuccess ||
+        hipHostMalloc((void **)&S.h_hb, 64, fl) != hipSuccess ||
         hipHostGetDevicePointer((void **)&S.d_rec, S.h_rec, 0) != hipSuccess ||
-        hipHostGetDevicePointer((void **)&S.d_res, S.h_res, 0) != hipSuccess)
+        hipHostGetDevicePointer((void **)&S.d_res, S.h_res, 0) != hipSuccess ||
+        hipHostGetDevicePointer((void **)&S.d_hb, S.h_hb, 0) != hipSuccess)
         return WC_ENOMEM;
     memset(S.h_rec, 0, wc::kSrvMaxPkts * sizeof(wc::SrvRec));
     memset((void *)S.h_res, 0, wc::kSrvMaxPkts * sizeof(wc::SrvRes));
+    memset(S.h_hb, 0, 64);
     S.ready = true;
     return WC_OK;
 }
 
-// Launch the grid over the records as they stand (the kernel serves any
-// record whose seq differs from seq0).  With `reset`, every record is first
-// rewritten to {seq, no stop}: nothing pending, stop flags cleared.
-int server_launch_locked(Device &D, int dev, bool reset, uint32_t seq0)
+// Launch the grid with every record rewritten to {S.seq, no stop} first:
+// nothing pending, stop flags cleared, the heartbeat at S.seq.
+int server_launch_locked(Device &D)
 {
     Server &S = D.srv;
-    if (reset)
-        for (uint32_t k = 0; k < wc::kSrvMaxPkts; ++k) {
-            S.h_rec[k].addr = 0;
-            S.h_rec[k].info = 0;
-            __atomic_store_n(&S.h_rec[k].seq, seq0, __ATOMIC_RELEASE);
-        }
-    (void)dev;
+    for (uint32_t k = 0; k < wc::kSrvMaxPkts; ++k) {
+        S.h_rec[k].addr = 0;
+        S.h_rec[k].info = 0;
+        __atomic_store_n(&S.h_rec[k].seq, S.seq, __ATOMIC_RELEASE);
+    }
+    __atomic_store_n(S.h_hb, S.seq, __ATOMIC_RELEASE);
     const uint64_t idle_ticks = kSrvSafetyMs * D.clock_khz;
-    const hipError_t e = wc::launch_serve(S.d_rec, S.d_res, seq0, S.waves, idle_ticks, S.st);
+    const hipError_t e =
+        wc::launch_serve(S.d_rec, S.d_res, S.d_hb, S.seq, S.waves, idle_ticks, S.st);
     if (e != hipSuccess)
         return hip_err(e);
     S.running = true;
+    S.posted = std::chrono::steady_clock::now();
+    ++g_srv_stats.launches;
     return WC_OK;
 }
 
@@ -874,19 +917,49 @@ void server_atexit()
     server_stop_all_locked();
 }
 
+// The next request number (0 is the records' initial value: never used).
+uint32_t server_next_seq(Server &S)
+{
+    S.seq = S.seq + 1 == 0 ? 1 : S.seq + 1;
+    return S.seq;
+}
+
+// Post request `seq`: the heartbeat first, then one record per packet, last
+// packet first -- a wave that sees its first record current finds every
+// later one of the request current too (stores become visible in program
+// order).
+void server_post(Server &S, uint32_t seq, const uint8_t *dbase, const uint64_t *h_off,
+                 const uint16_t *h_len, uint64_t n, uint32_t rkind)
+{
+    __atomic_store_n(S.h_hb, seq, __ATOMIC_RELEASE);
+    for (uint64_t k = n; k-- > 0;) {
+        wc::SrvRec &r = S.h_rec[k];
+        r.addr = (uint64_t)(dbase + h_off[k]) | (n << wc::kSrvAddrBits);
+        r.info = (uint32_t)h_len[k] | (rkind << 16);
+        __atomic_store_n(&r.seq, seq, __ATOMIC_RELEASE);
+    }
+    S.posted = std::chrono::steady_clock::now();
+}
+
 // One small registered batch through the server (caller holds g_mu, the
 // device is current).  Returns kSrvFallback when the server can't take it.
+// h_out2: the fused pair's header checksums (kind kKindFused).
 int serve_batch(Device &D, int dev, const uint8_t *dbase, const uint64_t *h_off,
-                const uint16_t *h_len, uint64_t n, uint8_t *h_out, int kind)
+                const uint16_t *h_len, uint64_t n, uint8_t *h_out, int kind,
+                uint16_t *h_out2 = nullptr)
 {
     Server &S = D.srv;
-    if (S.broken)
+    if (S.broken) {
+        ++g_srv_stats.fallbacks;
         return kSrvFallback;
+    }
     // The record packs the count above a 48-bit address: every packet's
     // (offsets come in any order).
     for (uint64_t k = 0; k < n; ++k)
-        if ((uint64_t)dbase + h_off[k] >= (1ull << wc::kSrvAddrBits))
+        if ((uint64_t)dbase + h_off[k] >= (1ull << wc::kSrvAddrBits)) {
+            ++g_srv_stats.fallbacks;
             return kSrvFallback;
+        }
     int rc = server_init_locked(S);
     if (rc)
         return rc;
@@ -895,27 +968,26 @@ int serve_batch(Device &D, int dev, const uint8_t *dbase, const uint64_t *h_off,
         g_srv_watcher = std::thread(server_watch);
         std::atexit(server_atexit);
     }
+    // A grid left without a request for half its own drain time is stopped
+    // and started afresh: it may be about to leave (each wave leaves once
+    // kSrvSafetyMs passed without a request it or the heartbeat showed), and
+    // a request posted to a grid that is half gone would not be answered in
+    // full.  (The idle watcher normally stops it within WC_SERVE_IDLE_US.)
+    if (S.running && std::chrono::steady_clock::now() - S.posted >
+                         std::chrono::milliseconds(kSrvSafetyMs / 2))
+        server_stop_locked(D, dev);
     if (!S.running) {
         S.waves = g_cfg.serve_waves;
-        rc = server_launch_locked(D, dev, true, S.seq);
+        rc = server_launch_locked(D);
         if (rc)
             return rc;
     }
-    uint32_t seq = S.seq + 1;
-    if (seq == 0) // 0 is the records' initial value
-        seq = 1;
-    S.seq = seq;
-    const uint32_t rkind = kind == kKindRx ? wc::kSrvKindRx : (uint32_t)kind;
-    // Last packet first: a wave that sees its first record current finds
-    // every later one of the request current too (stores become visible in
-    // program order).
-    for (uint64_t k = n; k-- > 0;) {
-        wc::SrvRec &r = S.h_rec[k];
-        r.addr = (uint64_t)(dbase + h_off[k]) | (n << wc::kSrvAddrBits);
-        r.info = (uint32_t)h_len[k] | (rkind << 16);
-        __atomic_store_n(&r.seq, seq, __ATOMIC_RELEASE);
-    }
-    const auto t0 = std::chrono::steady_clock::now();
+    const uint32_t rkind = kind == kKindRx      ? wc::kSrvKindRx
+                           : kind == kKindFused ? wc::kSrvKindFused
+                                                : (uint32_t)kind;
+    uint32_t seq = server_next_seq(S);
+    server_post(S, seq, dbase, h_off, h_len, n, rkind);
+    auto t0 = std::chrono::steady_clock::now();
     bool relaunched = false;
     for (uint64_t k = 0; k < n; ++k) {
         for (uint32_t spin = 1;; ++spin) {
@@ -927,16 +999,26 @@ int serve_batch(Device &D, int dev, const uint8_t *dbase, const uint64_t *h_off,
             const auto dt = std::chrono::steady_clock::now() - t0;
             if (dt > std::chrono::milliseconds(50) && !relaunched &&
                 hipStreamQuery(S.st) == hipSuccess) {
-                // the grid had drained (its own idle limit): serve again
+                // The grid is gone (it cannot leave part-way: see above):
+                // start it afresh -- every record reset, so no wave takes a
+                // stale record for a request -- and post the batch again.
                 relaunched = true;
-                rc = server_launch_locked(D, dev, false, seq - 1);
+                S.running = false;
+                rc = server_launch_locked(D);
                 if (rc)
                     return rc;
+                seq = server_next_seq(S);
+                server_post(S, seq, dbase, h_off, h_len, n, rkind);
+                t0 = std::chrono::steady_clock::now();
+                k = 0;
+                spin = 0;
+                continue;
             }
             if (dt > std::chrono::milliseconds(2000)) {
                 fprintf(stderr, "wccksum: resident server did not answer; using launches\n");
                 server_stop_locked(D, dev);
                 S.broken = true;
+                ++g_srv_stats.fallbacks;
                 return kSrvFallback;
             }
         }
@@ -948,14 +1030,19 @@ int serve_batch(Device &D, int dev, const uint8_t *dbase, const uint64_t *h_off,
         uint16_t *o = (uint16_t *)h_out;
         for (uint64_t k = 0; k < n; ++k)
             o[k] = (uint16_t)S.h_res[k].value;
+        if (kind == kKindFused)
+            for (uint64_t k = 0; k < n; ++k)
+                h_out2[k] = (uint16_t)(S.h_res[k].value >> 16);
     }
     S.last = std::chrono::steady_clock::now();
+    ++g_srv_stats.served;
     return WC_OK;
 }
 
 // Small registered batch: one launch reading host memory in place.
 int host_zero_copy(Device &D, const uint8_t *dbase, const uint64_t *h_off,
-                   const uint16_t *h_len, uint64_t n, uint8_t *h_out, int kind)
+                   const uint16_t *h_len, uint64_t n, uint8_t *h_out, int kind,
+                   uint16_t *h_out2 = nullptr)
 {
     int rc = zc_init_locked(D);
     if (rc)
@@ -963,13 +1050,16 @@ int host_zero_copy(Device &D, const uint8_t *dbase, const uint64_t *h_off,
     ZeroCopy &Z = D.zc;
     memcpy(Z.h_off, h_off, n * 8);
     memcpy(Z.h_len, h_len, n * 2);
-    rc = run_ragged_any(D, g_cfg, dbase, Z.d_off, Z.d_len, n, Z.d_out, kind, true, Z.st);
+    rc = run_ragged_any(D, g_cfg, dbase, Z.d_off, Z.d_len, n, Z.d_out, kind, true, Z.st,
+                        Z.d_out2);
     if (rc)
         return rc;
     hipError_t e = hipStreamSynchronize(Z.st);
     if (e != hipSuccess)
         return hip_err(e);
     memcpy(h_out, (const void *)Z.h_out, n * out_size(kind));
+    if (kind == kKindFused)
+        memcpy(h_out2, (const void *)Z.h_out2, n * 2);
     return WC_OK;
 }
 
@@ -1104,6 +1194,7 @@ struct PipeRun {
     const uint64_t *h_off = nullptr;
     const uint16_t *h_len = nullptr;
     uint8_t *h_out = nullptr; // out_size(kind) bytes per packet
+    uint16_t *h_out2 = nullptr; // fused pair: the header checksums
     int kind = WC_CKSUM_IP;
     uint64_t i = 0, hi = 0;
     uint64_t pend_lo[kPipe] = {}, pend_n[kPipe] = {};
@@ -1111,6 +1202,12 @@ struct PipeRun {
     int slot = 0;
 
     bool done() const { return i >= hi; }
+
+    // Bytes packet j's check reads (the fused pair: also its IPv4 header).
+    uint64_t span(uint64_t j) const
+    {
+        return kind == kKindFused ? fused_span(hb + h_off[j], h_len[j]) : span_of(h_len[j], kind);
+    }
 
     // Wait for a slot's chunk and copy its results out.
     int drain(int s)
@@ -1122,6 +1219,8 @@ struct PipeRun {
             return hip_err(e);
         const int osz = out_size(kind);
         memcpy(h_out + pend_lo[s] * osz, P->h_out[s], pend_n[s] * osz);
+        if (kind == kKindFused)
+            memcpy(h_out2 + pend_lo[s], P->h_out2[s], pend_n[s] * 2);
         pend[s] = false;
         return WC_OK;
     }
@@ -1151,7 +1250,7 @@ struct PipeRun {
             const uint64_t lo = h_off[i];
             uint64_t top = lo;
             while (j < hi && j - i0 < kChunkPkts) {
-                const uint64_t e = h_off[j] + span_of(h_len[j], kind);
+                const uint64_t e = h_off[j] + span(j);
                 if (std::max(top, e) - lo > kChunkBytes && j > i0)
                     break;
                 top = std::max(top, e);
@@ -1169,7 +1268,7 @@ struct PipeRun {
             // Rebased offsets first (a prefix sum), then the packet copies
             // in parallel ranges of the staging pool.
             while (j < hi && j - i0 < kChunkPkts) {
-                const uint64_t sp = span_of(h_len[j], kind);
+                const uint64_t sp = span(j);
                 if (bytes + sp > kChunkBytes && j > i0)
                     break;
                 P->h_off[slot][j - i0] = bytes;
@@ -1186,7 +1285,7 @@ struct PipeRun {
                 const uint64_t a = cnt * (uint64_t)t / (uint64_t)parts;
                 const uint64_t b = cnt * (uint64_t)(t + 1) / (uint64_t)parts;
                 for (uint64_t q = a; q < b; ++q)
-                    memcpy(dst + roff[q], hb + h_off[i0 + q], span_of(h_len[i0 + q], kind));
+                    memcpy(dst + roff[q], hb + h_off[i0 + q], span(i0 + q));
             };
             pool.run(std::max(parts, 1), gather);
             src = P->h_bytes[slot];
@@ -1203,11 +1302,14 @@ struct PipeRun {
         if (e != hipSuccess)
             return hip_err(e);
         rc = run_ragged_any(*D, g_cfg, P->d_bytes[slot], P->d_off[slot], P->d_len[slot], cnt,
-                            P->d_out[slot], kind, false, st);
+                            P->d_out[slot], kind, false, st, P->d_out2[slot]);
         if (rc)
             return rc;
         e = hipMemcpyAsync(P->h_out[slot], P->d_out[slot], cnt * out_size(kind),
                            hipMemcpyDeviceToHost, st);
+        if (e == hipSuccess && kind == kKindFused)
+            e = hipMemcpyAsync(P->h_out2[slot], P->d_out2[slot], cnt * 2, hipMemcpyDeviceToHost,
+                               st);
         if (e == hipSuccess)
             e = hipEventRecord(P->done[slot], st);
         if (e != hipSuccess)
@@ -1232,16 +1334,21 @@ struct PipeRun {
 };
 
 // Every packet of a host batch inside [0, h_bytes); its order and bytes.
-bool host_batch_ok(uint64_t h_bytes, const uint64_t *h_off, const uint16_t *h_len, uint64_t n,
-                   int kind, bool *ascending, uint64_t *total)
+bool host_batch_ok(const uint8_t *hb, uint64_t h_bytes, const uint64_t *h_off,
+                   const uint16_t *h_len, uint64_t n, int kind, bool *ascending, uint64_t *total)
 {
     bool asc = true;
     uint64_t tot = 0;
     for (uint64_t i = 0; i < n; ++i) {
         const uint64_t o = h_off[i];
-        const uint64_t sp = span_of(h_len[i], kind);
+        uint64_t sp = span_of(h_len[i], kind);
         if (o > h_bytes || sp > h_bytes - o)
             return false;
+        if (kind == kKindFused) { // (its first sp >= 20 bytes are in range)
+            sp = fused_span(hb + o, h_len[i]);
+            if (sp > h_bytes - o)
+                return false;
+        }
         asc &= i == 0 || o >= h_off[i - 1];
         tot += sp;
     }
@@ -1259,7 +1366,7 @@ void shard_range(uint64_t n, int g, int G, uint64_t *lo, uint64_t *hi)
 
 int host_pipeline(Device &D, const uint8_t *hb, bool registered, bool ascending,
                   const uint64_t *h_off, const uint16_t *h_len, uint64_t n,
-                  uint8_t *h_out, int kind)
+                  uint8_t *h_out, int kind, uint16_t *h_out2)
 {
     PipeRun r;
     r.D = &D;
@@ -1270,6 +1377,7 @@ int host_pipeline(Device &D, const uint8_t *hb, bool registered, bool ascending,
     r.h_off = h_off;
     r.h_len = h_len;
     r.h_out = h_out;
+    r.h_out2 = h_out2;
     r.kind = kind;
     r.hi = n;
     while (!r.done()) {
@@ -1311,18 +1419,22 @@ int for_each_shard(F &&fn)
     return rc;
 }
 
-// wc_cksum_host / wc_rx_verdict_host: a host-memory batch on the current
-// device -- zero-copy for a small registered batch, else the pipeline.
+// wc_cksum_host / wc_rx_verdict_host / wc_cksum_ip_udp_host: a host-memory
+// batch on the current device -- the resident server or one zero-copy launch
+// for a small registered batch, else the pipeline.  h_out2: the fused pair's
+// header checksums.
 int host_batch(const void *h_base, uint64_t h_bytes, const uint64_t *h_off,
-               const uint16_t *h_len, uint64_t n, uint8_t *h_out, int kind)
+               const uint16_t *h_len, uint64_t n, uint8_t *h_out, int kind,
+               uint16_t *h_out2 = nullptr)
 {
     if (n == 0)
         return WC_OK;
-    if (!h_base || !h_off || !h_len || !h_out)
+    if (!h_base || !h_off || !h_len || !h_out || (kind == kKindFused && !h_out2))
         return WC_EINVAL;
     bool ascending = true;
     uint64_t total = 0;
-    if (!host_batch_ok(h_bytes, h_off, h_len, n, kind, &ascending, &total))
+    if (!host_batch_ok((const uint8_t *)h_base, h_bytes, h_off, h_len, n, kind, &ascending,
+                       &total))
         return WC_EINVAL;
 
     std::lock_guard<std::mutex> lk(g_mu);
@@ -1332,23 +1444,23 @@ int host_batch(const void *h_base, uint64_t h_bytes, const uint64_t *h_off,
         return rc;
     const uint8_t *dbase = registered_dptr_locked(h_base, h_bytes);
     if (dbase && g_cfg.serve && n <= (uint64_t)g_cfg.serve_max) {
-        bool fits = true;
+        bool fits = true; // (a fused header adds at most 40 bytes to the span)
         for (uint64_t i = 0; i < n && fits; ++i)
-            fits = span_of(h_len[i], kind) <= wc::kSrvMaxBytes;
+            fits = span_of(h_len[i], kind) + (kind == kKindFused ? 40u : 0u) <= wc::kSrvMaxBytes;
         int dev = 0;
         if (fits && current_device(&dev) == WC_OK) {
-            rc = serve_batch(*D, dev, dbase, h_off, h_len, n, h_out, kind);
+            rc = serve_batch(*D, dev, dbase, h_off, h_len, n, h_out, kind, h_out2);
             if (rc != kSrvFallback)
                 return rc;
         }
     }
     if (dbase && n <= kZcPkts && total <= (uint64_t)g_cfg.zc_bytes)
-        return host_zero_copy(*D, dbase, h_off, h_len, n, h_out, kind);
+        return host_zero_copy(*D, dbase, h_off, h_len, n, h_out, kind, h_out2);
     rc = pipe_init_locked(D->pipe);
     if (rc)
         return rc;
     return host_pipeline(*D, (const uint8_t *)h_base, dbase != nullptr, ascending,
-                         h_off, h_len, n, h_out, kind);
+                         h_off, h_len, n, h_out, kind, h_out2);
 }
 
 } // namespace
@@ -1432,6 +1544,11 @@ int wc_host_register(void *h_ptr, uint64_t bytes)
     int rc = init_locked(-1, &D);
     if (rc)
         return rc;
+    // The resident server grid would hold up a device-wide synchronisation
+    // that (un)registering may do until the idle watcher stopped it -- and
+    // the watcher waits for g_mu, held here.  Stop it first; the next small
+    // call starts it again.
+    server_stop_all_locked();
     // Registering a base address again always pins the pages mapped there
     // NOW: the caller may have freed the old region without
     // wc_host_unregister and got a new buffer at the same address, whose
@@ -1481,6 +1598,7 @@ int wc_host_unregister(void *h_ptr)
     if (it == g_registered.end())
         return WC_EINVAL;
     g_registered.erase(it);
+    server_stop_all_locked(); // (see wc_host_register)
     return hip_err(hipHostUnregister(h_ptr));
 }
 
@@ -1490,6 +1608,28 @@ int wc_cksum_host(const void *h_base, uint64_t h_bytes, const uint64_t *h_off,
     if (kind != WC_CKSUM_IP && kind != WC_CKSUM_PAYLOAD)
         return WC_EINVAL;
     return host_batch(h_base, h_bytes, h_off, h_len, n, (uint8_t *)h_out, kind);
+}
+
+int wc_cksum_ip_udp_host(const void *h_base, uint64_t h_bytes, const uint64_t *h_off,
+                         const uint16_t *h_len, uint64_t n, uint16_t *h_out_ip_hdr,
+                         uint16_t *h_out_payload)
+{
+    if (n && (!h_out_ip_hdr || !h_out_payload))
+        return WC_EINVAL;
+    return host_batch(h_base, h_bytes, h_off, h_len, n, (uint8_t *)h_out_payload, kKindFused,
+                      h_out_ip_hdr);
+}
+
+int wc_server_stats(uint64_t *served, uint64_t *fallbacks, uint64_t *launches)
+{
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (served)
+        *served = g_srv_stats.served;
+    if (fallbacks)
+        *fallbacks = g_srv_stats.fallbacks;
+    if (launches)
+        *launches = g_srv_stats.launches;
+    return WC_OK;
 }
 
 int wc_rx_verdict_ragged(const void *d_base, const uint64_t *d_off, const uint16_t *d_frame_len,
@@ -1618,7 +1758,8 @@ int wc_cksum_host_multi(const void *h_base, uint64_t h_bytes, const uint64_t *h_
         return wc_cksum_host(h_base, h_bytes, h_off, h_len, n, h_out, kind);
     bool ascending = true;
     uint64_t total = 0;
-    if (!host_batch_ok(h_bytes, h_off, h_len, n, kind, &ascending, &total))
+    if (!host_batch_ok((const uint8_t *)h_base, h_bytes, h_off, h_len, n, kind, &ascending,
+                       &total))
         return WC_EINVAL;
     {
         std::lock_guard<std::mutex> lk(g_mu);
@@ -1760,11 +1901,13 @@ int wc_gpu_fini(void)
             (void)hipHostFree(D.zc.h_off);
             (void)hipHostFree(D.zc.h_len);
             (void)hipHostFree(D.zc.h_out);
+            (void)hipHostFree(D.zc.h_out2);
         }
         if (D.srv.ready) {
             (void)hipStreamDestroy(D.srv.st);
             (void)hipHostFree(D.srv.h_rec);
             (void)hipHostFree(D.srv.h_res);
+            (void)hipHostFree(D.srv.h_hb);
         }
         (void)hipStreamSynchronize(D.scalar_st);
         (void)hipStreamDestroy(D.scalar_st);

@@ -180,6 +180,10 @@ hipError_t launch_rx_verdict(const void *base, const uint64_t *offs, const uint1
 constexpr uint32_t kSrvMaxPkts = 1024;  // packets per request
 constexpr uint32_t kSrvMaxBytes = 4064; // bytes one packet (frame) may span
 constexpr uint32_t kSrvKindRx = 2;      // record kind beside WC_KIND_IP / _PAYLOAD
+// Fused TX record: payload_cksum(pkt, len) | ip_cksum(pkt, ip4_hl) << 16 (0
+// for IPv6), the two checksums mk_ip4_hdr + udp_tx compute (ip4.c:184-186,
+// udp.c:209-213).
+constexpr uint32_t kSrvKindFused = 3;
 constexpr int kSrvAddrBits = 48;        // the packet count rides above the address
 struct alignas(16) SrvRec {
     uint64_t addr; // device address of the packet / frame (< 2^48) | n << 48
@@ -190,7 +194,10 @@ struct alignas(8) SrvRes {
     uint32_t value; // checksum or RX verdict
     uint32_t seq;   // the request it answers
 };
-hipError_t launch_serve(const SrvRec *d_recs, SrvRes *d_res, uint32_t seq0, int waves,
-                        uint64_t idle_ticks, hipStream_t st);
+// d_hb: the host's heartbeat word (the latest request number, written before
+// every request's records): a wave leaves on its own only after idle_ticks in
+// which the heartbeat did not move, so the grid drains as a whole.
+hipError_t launch_serve(const SrvRec *d_recs, SrvRes *d_res, const uint32_t *d_hb, uint32_t seq0,
+                        int waves, uint64_t idle_ticks, hipStream_t st);
 
 } // namespace wc

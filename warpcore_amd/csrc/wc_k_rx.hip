@@ -434,7 +434,9 @@ hipError_t launch_rx_verdict(const void *base, const uint64_t *offs, const uint1
     const uint64_t tiles = (n + 63) / 64;
     const int grid = (int)std::min<uint64_t>(
         kMaxGridBlocks, std::max<uint64_t>(1, (tiles + kFlatWaves - 1) / kFlatWaves));
-    const bool early = mode & kRxEarly, ht = mode & kRxHdrT, skip = mode & kRxSkip;
+    // EARLY streams only the checked frames: SKIP has nothing to skip there,
+    // and is dropped so that NT and HDRT are still honoured
+    const bool early = mode & kRxEarly, ht = mode & kRxHdrT, skip = (mode & kRxSkip) && !early;
 #define WC_RX(N, E, H, S)                                                      \
     if (nt == N && early == E && ht == H && skip == S)                         \
         return launch_rx_one<N, E, H, S>(base, offs, flens, n, verdict, drops, grid, st);
@@ -446,8 +448,7 @@ hipError_t launch_rx_verdict(const void *base, const uint64_t *offs, const uint1
     WC_RX_NT(false)
 #undef WC_RX_NT
 #undef WC_RX
-    // EARLY streams only the checked frames: SKIP has nothing to skip
-    return launch_rx_one<true, true, true, false>(base, offs, flens, n, verdict, drops, grid, st);
+    return hipErrorInvalidValue; // (every combination is listed above)
 }
 
 } // namespace wc

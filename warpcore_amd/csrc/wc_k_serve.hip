@@ -22,13 +22,19 @@
 //     {result, seq} to the packet's 8-byte result slot in mapped host memory
 //     with one system-scope store;
 //   * the host spins on the n result slots.
-// Kinds: ip_cksum, payload_cksum, and the RX verdict of an Ethernet frame
+// Kinds: ip_cksum, payload_cksum, the RX verdict of an Ethernet frame
 // (eth_rx -> ip4_rx / ip6_rx -> udp_rx: eth.c:75-86, ip4.c:95-138,
 // ip6.c:91-111, udp.c:99-139; the same decisions, in the same order, as
-// k_rx_verdict and oracle_rx_verdict).
+// k_rx_verdict and oracle_rx_verdict), and the fused TX pair --
+// payload_cksum and the IPv4 header's ip_cksum of one packet from one read
+// of its bytes (mk_ip4_hdr + udp_tx, ip4.c:184-186, udp.c:209-213).
 // Exit: every wave leaves when its record carries the stop flag (the host's
-// idle watcher and wc_gpu_fini set it) or after `idle_ticks` of the wall
-// clock without a request -- so the grid always drains.
+// idle watcher, wc_gpu_fini, a host-side restart set it), or once the wall
+// clock has run `idle_ticks` past the last request ANY wave saw: a wave whose
+// own records stayed quiet re-reads the host's heartbeat word (the latest
+// request number) before it leaves, so light traffic that never reaches a
+// wave does not thin the grid out -- the grid drains as a whole, and always
+// drains.
 #include "wc_device.h"
 
 namespace wc {
@@ -51,6 +57,17 @@ __device__ __forceinline__ u32x4 load_sys16(const void *p)
                  : "v"(p)
                  : "memory");
     return v;
+}
+
+// One host word past every cache: the heartbeat.
+__device__ __forceinline__ uint32_t load_sys4(const uint32_t *p)
+{
+    uint32_t v;
+    asm volatile("global_load_dword %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)"
+                 : "=v"(v)
+                 : "v"(p)
+                 : "memory");
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)v);
 }
 
 struct Rec {
@@ -128,7 +145,7 @@ __device__ __forceinline__ uint32_t sv_sum(const u32x4 (&d)[kSvLoads], uint32_t 
 // up to byte 19 whatever len is (in_cksum.c:149-151); an RX frame its length.
 __device__ __forceinline__ uint32_t sv_span(uint32_t len, uint32_t kind)
 {
-    return kind == WC_KIND_PAYLOAD ? max(len, 20u) : len;
+    return kind == WC_KIND_PAYLOAD || kind == kSrvKindFused ? max(len, 20u) : len;
 }
 
 // ip_cksum / payload_cksum of [a, a + len) (in_cksum.c:133-167) from its
@@ -143,6 +160,33 @@ __device__ __forceinline__ uint32_t sv_cksum(const u32x4 (&d)[kSvLoads], uint64_
         pseudo_hdr(sv_byte(d, s, 0), sv_byte(d, s, 2), sv_byte(d, s, 3), sv_byte(d, s, 6));
     return fold_not(sv_sum<WC_KIND_PAYLOAD>(d, s, lane, (int)ph.hl, (int)len, ph.v4, a & 1u) +
                     ph.special);
+}
+
+// The fused TX pair of packet [a, a + len): payload_cksum(pkt, len) in the
+// low half, ip_cksum(pkt, hl) of an IPv4 header in the high half (0 for
+// IPv6, which has no header checksum) -- what mk_ip4_hdr and udp_tx store
+// (ip4.c:184-186, udp.c:209-213).  An IPv4 header longer than the bytes
+// loaded with the packet (options past a short len) is loaded again on its
+// own (rare: the host checked [a, a + hl) lies in the region).
+__device__ __forceinline__ uint32_t sv_fused(const u32x4 (&d)[kSvLoads], uint64_t a, uint32_t len,
+                                             int lane)
+{
+    const uint32_t s = (uint32_t)__builtin_amdgcn_readfirstlane((int)(a & 15u));
+    const PseudoHdr ph =
+        pseudo_hdr(sv_byte(d, s, 0), sv_byte(d, s, 2), sv_byte(d, s, 3), sv_byte(d, s, 6));
+    const uint32_t pay = fold_not(
+        sv_sum<WC_KIND_PAYLOAD>(d, s, lane, (int)ph.hl, (int)len, ph.v4, a & 1u) + ph.special);
+    if (!ph.v4)
+        return pay;
+    uint32_t hs;
+    if (ph.hl <= max(len, 20u)) {
+        hs = sv_sum<WC_KIND_IP>(d, s, lane, 0, (int)ph.hl, 0u, a & 1u);
+    } else {
+        u32x4 e[kSvLoads];
+        sv_load(a, ph.hl, lane, e);
+        hs = sv_sum<WC_KIND_IP>(e, s, lane, 0, (int)ph.hl, 0u, a & 1u);
+    }
+    return pay | ((uint32_t)fold_not(hs) << 16);
 }
 
 // The RX verdict of frame [fa, fa + flen), the reference's check order
@@ -207,20 +251,31 @@ __device__ __forceinline__ uint32_t sv_rx(const u32x4 (&d)[kSvLoads], uint64_t f
 }
 
 __global__ void __launch_bounds__(64) k_serve(const SrvRec *__restrict__ recs,
-                                              SrvRes *__restrict__ res, uint32_t seq0,
+                                              SrvRes *__restrict__ res,
+                                              const uint32_t *__restrict__ hb, uint32_t seq0,
                                               uint64_t idle_ticks)
 {
     const int lane = threadIdx.x;
     const uint32_t w = blockIdx.x, W = gridDim.x;
-    uint32_t last = seq0;
+    uint32_t last = seq0, hb_seen = seq0;
     uint64_t t_last = (uint64_t)wall_clock64();
     for (;;) {
         Rec r = rec_load(&recs[w]);
         if (r.stop)
             return;
         if (r.seq == last) {
-            if ((uint64_t)wall_clock64() - t_last > idle_ticks)
-                return; // nobody asked for idle_ticks: drain
+            const uint64_t now = (uint64_t)wall_clock64();
+            if (now - t_last > idle_ticks) {
+                // Quiet for idle_ticks here; leave only if the whole grid
+                // was (no request since this wave last looked), else keep
+                // serving: a wave that exits while the others stay would
+                // leave its share of a later, larger request unanswered.
+                const uint32_t h = load_sys4(hb);
+                if (h == hb_seen)
+                    return;
+                hb_seen = h;
+                t_last = now;
+            }
             __builtin_amdgcn_s_sleep(2);
             continue;
         }
@@ -276,9 +331,10 @@ __global__ void __launch_bounds__(64) k_serve(const SrvRec *__restrict__ recs,
                 if (two)
                     sv_load(r1.addr, sv_span(r1.len, r1.kind), lane, d1);
                 auto answer = [&](const Rec &x, const u32x4 (&d)[kSvLoads], uint32_t k) {
-                    const uint32_t v = x.kind == kSrvKindRx
-                                           ? sv_rx(d, x.addr, x.len, lane)
-                                           : sv_cksum(d, x.addr, x.len, x.kind, lane);
+                    const uint32_t v = x.kind == kSrvKindRx      ? sv_rx(d, x.addr, x.len, lane)
+                                       : x.kind == kSrvKindFused ? sv_fused(d, x.addr, x.len, lane)
+                                                                 : sv_cksum(d, x.addr, x.len,
+                                                                            x.kind, lane);
                     if (lane == 0)
                         __hip_atomic_store((uint64_t *)&res[k],
                                            (uint64_t)v | ((uint64_t)seq << 32), __ATOMIC_RELAXED,
@@ -312,10 +368,11 @@ __global__ void __launch_bounds__(64) k_serve(const SrvRec *__restrict__ recs,
 
 } // namespace
 
-hipError_t launch_serve(const SrvRec *d_recs, SrvRes *d_res, uint32_t seq0, int waves,
-                        uint64_t idle_ticks, hipStream_t st)
+hipError_t launch_serve(const SrvRec *d_recs, SrvRes *d_res, const uint32_t *d_hb, uint32_t seq0,
+                        int waves, uint64_t idle_ticks, hipStream_t st)
 {
-    hipLaunchKernelGGL(k_serve, dim3(waves), dim3(64), 0, st, d_recs, d_res, seq0, idle_ticks);
+    hipLaunchKernelGGL(k_serve, dim3(waves), dim3(64), 0, st, d_recs, d_res, d_hb, seq0,
+                       idle_ticks);
     return hipGetLastError();
 }
 
