@@ -140,17 +140,17 @@ PLANNED = [
     (0, 256, 256, "ip", (8, 2, 2)),           # lean kernel, the pass filled exactly
     (0, 576, 576, "ip", (16, 3, 1)),
     (0, 9000, 9000, "ip", (32, 18, 1)),
-    (14, 2048, 64, "ip", (8, 1, 4)),          # small packets in netmap slots
-    (14, 2048, 64, "payload", (4, 2, 2)),
-    (14, 2048, 128, "ip", (8, 3, 2)),
-    (14, 2048, 128, "payload", (4, 2, 2)),    # sparse payload, 7..16 chunks
-    (14, 2048, 240, "payload", (4, 2, 2)),
+    (14, 2048, 64, "ip", (8, 1, 4)),          # small packets in netmap slots (lean, PH)
+    (14, 2048, 64, "payload", (8, 1, 4)),
+    (14, 2048, 128, "ip", (8, 2, 4)),
+    (14, 2048, 128, "payload", (8, 2, 4)),
+    (14, 2048, 240, "payload", (8, 2, 4)),
 ]
 
 
 @pytest.mark.parametrize("base,stride,length,kind,shape", PLANNED)
 def test_planner_shapes(gpu, monkeypatch, base, stride, length, kind, shape):
-    for k in ("WC_SHAPE", "WC_STRIDED_SEG", "WC_VARIANT", "WC_LEAN_MAX"):
+    for k in ("WC_SHAPE", "WC_STRIDED_SEG", "WC_VARIANT", "WC_LEAN_MAX", "WC_LEAN_PHASE"):
         monkeypatch.delenv(k, raising=False)
     wc.reload_config()
     p = wc.plan_strided(0x100000000 + base, stride, length, 1 << 20, kind=kind)
@@ -447,6 +447,49 @@ def test_payload_strided_netmap_layout(gpu):
                                     byte_offset=14))
         want = c_oracle.cksum_strided(buf, slot, 1500, n, kind=1, byte_offset=14)
         np.testing.assert_array_equal(got, want)
+
+
+PHASE_LENS = [1, 2, 15, 20, 47, 48, 49, 63, 64, 65, 100, 127, 128, 129, 200, 255, 256,
+              300, 511, 600, 700, 750]
+
+
+@pytest.mark.parametrize("lean_phase", ["1", "0"])
+@pytest.mark.parametrize("length", PHASE_LENS)
+def test_lean_phase_slots(gpu, monkeypatch, length, lean_phase):
+    """Sparse packets at an even start phase (netmap slots, IP header at +14)
+    on the lean kernel's PH path (per-slot byte masks, header words by DPP)
+    and, with WC_LEAN_PHASE=0, on the group kernel: both kinds, phases 2 / 6 /
+    14, a tail wave, and payload headers of every shape -- IPv4 with IHL 5,
+    options (IHL 15), malformed IHL 1, IPv6 with next header 254 / 255."""
+    monkeypatch.setenv("WC_LEAN_PHASE", lean_phase)
+    wc.reload_config()
+    rng = np.random.default_rng(length * 7 + int(lean_phase))
+    n, stride = 333, 2048
+    buf = rng.integers(0, 256, n * stride + 64, dtype=np.uint8)
+    for start in (2, 6, 14):
+        b = buf.copy()
+        for i in range(n):
+            o = start + i * stride
+            k = i % 5
+            if k == 0 and length >= 60:
+                b[o] = 0x4F
+            elif k == 1:
+                b[o] = 0x41
+            elif k == 2:
+                b[o] = 0x60
+                if length > 6:
+                    b[o + 6] = 254 + (i & 1)
+            elif k == 3:
+                b[o] = 0x45
+        d = dev_u8(b, gpu)
+        for kind, kn in (("ip", 0), ("payload", 1)):
+            if kind == "payload" and length < 20:
+                continue
+            got = host(wc.cksum_strided(d, stride, length, n, kind=kind, byte_offset=start))
+            want = c_oracle.cksum_strided(b, stride, length, n, kind=kn, byte_offset=start)
+            np.testing.assert_array_equal(got, want, err_msg=f"{kind} start {start}")
+    plan = wc.plan_strided(0x100000000 + 14, stride, length, n, kind="ip")
+    assert (plan["kernel"] == "lean") == (lean_phase == "1" and length <= 48 * 16 - 14 - 15)
 
 
 @pytest.mark.parametrize("length", [60, 64, 100, 333, 1000, 1500])

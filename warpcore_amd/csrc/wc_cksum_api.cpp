@@ -154,6 +154,7 @@ struct Config {
     int flat_pk = 1;               // WC_FLAT_PK: flat kernel chunks per lane slot
     int gather = 1;                // WC_GATHER: seg kernel's gathered-stream path (0 off, 2 forced)
     int lean_max = 48;             // WC_LEAN_MAX: lean kernel for aligned packets up to this many chunks
+    int lean_phase = 1;            // WC_LEAN_PHASE: lean kernel for sparse packets at an even phase too
     int serve = 1;                 // WC_SERVE: resident server for small registered host batches
     int serve_waves = 64;          // WC_SERVE_WAVES: its waves (one 64-lane workgroup each)
     int serve_max = 256;           // WC_SERVE_MAX: largest batch (packets) it takes
@@ -248,6 +249,7 @@ void load_config_locked()
     c.flat_pk = env_int("WC_FLAT_PK", c.flat_pk);
     c.gather = env_int("WC_GATHER", c.gather);
     c.lean_max = env_int("WC_LEAN_MAX", c.lean_max);
+    c.lean_phase = env_int("WC_LEAN_PHASE", c.lean_phase);
     c.serve = env_int("WC_SERVE", c.serve);
     c.serve_waves = std::max(1, std::min(env_int("WC_SERVE_WAVES", c.serve_waves), 1024));
     c.serve_max = std::max(0, std::min(env_int("WC_SERVE_MAX", c.serve_max), (int)wc::kSrvMaxPkts));
@@ -417,6 +419,25 @@ wc::Shape shape_for_chunks(uint32_t nch, bool full, bool payload, bool aligned,
 // as one contiguous kilobyte per load; ~4 loads in flight per lane
 // (profiles/ab_r03_lean*.log).  {0,0,0}: no such shape, not lean.  Packets
 // under 4 chunks take the masked path of (4, 1, 4).
+// Lean-kernel shape for packets at a start phase (PH): one pass covering the
+// window, dead slots allowed (they read nothing new and are masked).
+wc::Shape lean_ph_shape(uint32_t nch)
+{
+    if (nch <= 4)
+        return {4, 1, 4};
+    if (nch <= 8)
+        return {8, 1, 4};
+    if (nch <= 16)
+        return {8, 2, 4};
+    if (nch <= 24)
+        return {8, 3, 2};
+    if (nch <= 32)
+        return {16, 2, 2};
+    if (nch <= 48)
+        return {16, 3, 1};
+    return {0, 0, 0};
+}
+
 wc::Shape lean_shape_for(uint32_t nch)
 {
     if (nch <= 4)
@@ -526,9 +547,14 @@ Plan plan_strided(const Device &D, const Config &C, uint64_t base, uint64_t stri
     // first lane.  payload_cksum needs len >= 48 there (the whole IPv4 /
     // IPv6 header inside the packet); up to WC_LEAN_MAX chunks.
     const bool aligned16 = base % 16 == 0 && stride % 16 == 0 && len % 16 == 0 && len != 0;
-    if (!hdr && C.lean_max > 0 && aligned16 && (!payload || len >= 48) &&
+    // Sparse packets at one even start phase (netmap slots: IP packets at
+    // +14) take it too, with per-slot byte masks (PH, wc_k_lean.hip).
+    const bool phased = !aligned16 && C.lean_phase && C.nt && stride % 16 == 0 &&
+                        base % 2 == 0 && len != 0 && !packed && sseg != 2;
+    if (!hdr && C.lean_max > 0 && (aligned16 || phased) && (!payload || len >= 48) &&
         nch <= (uint32_t)C.lean_max && (sseg != 2 || !packed)) {
-        const wc::Shape sh = C.have_shape ? C.shape : lean_shape_for(nch);
+        const wc::Shape sh = C.have_shape ? C.shape : aligned16 ? lean_shape_for(nch)
+                                                                 : lean_ph_shape(nch);
         const uint64_t ppw = (uint64_t)(64 / std::max(sh.group, 1)) * sh.unroll;
         if (lean_shape_ok(sh) && nch <= (uint32_t)(sh.group * sh.cpl) && ppw <= 64 &&
             ppw * stride < (1ull << 32)) {

@@ -56,10 +56,27 @@ __device__ __forceinline__ uint32_t lean_extra(const u32x4 &c, bool &ok)
                  : ph.special + (c.y & 0xFFFFu);
 }
 
-template <int G, int CPL, int U, int KIND, bool NT>
+// Bytes [lo, hi) of a dword whose first byte is window byte b, as a mask.
+__device__ __forceinline__ uint32_t range_mask(int b, int lo, int hi)
+{
+    const int l = min(max(lo - b, 0), 4), h = min(max(hi - b, 0), 4);
+    return (uint32_t)(((1ull << (8 * h)) - 1ull) & ~((1ull << (8 * l)) - 1ull));
+}
+
+// PH: the packets share an even start phase p != 0 in their 16-byte chunks
+// (stride % 16 == 0, e.g. IP packets at +14 in netmap slots), and / or len is
+// not a multiple of 16.  The wave then reads each packet's chunk-aligned
+// window [a - p, a - p + 16 nch), and every lane ANDs its chunks with masks
+// that are the same for every packet -- computed once per kernel -- before
+// the word sums: with an even phase the window's little-endian words are the
+// packet's, and a masked odd tail byte is its low byte, as in_cksum.c:107-120
+// adds it.  payload_cksum's header words (packet bytes 0..11) come from the
+// unmasked window dwords of group lanes 0 and 1, one DPP broadcast each.
+template <int G, int CPL, int U, int KIND, bool NT, bool PH>
 __global__ void __launch_bounds__(256)
 k_cksum_lean(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len, uint64_t n,
-             uint16_t *__restrict__ out, unsigned long long *__restrict__ bad, int variant_arg)
+             uint16_t *__restrict__ out, unsigned long long *__restrict__ bad, int variant_arg,
+             uint32_t phase)
 {
     const int variant = tuning_variant(variant_arg); // 0 outside the tuning build
     constexpr int GPW = 64 / G;
@@ -74,15 +91,27 @@ k_cksum_lean(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len, ui
     // Wave-uniform in SGPRs: the wave index and so the first packet's address.
     const uint32_t wib = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint64_t nwaves = (uint64_t)gridDim.x * 4u;
-    const uint32_t nch = len >> 4;
-    const bool fills = nch == PASS; // uniform: every chunk slot holds packet bytes
+    const uint32_t ph = PH ? phase : 0u;
+    const uint32_t nch = PH ? (ph + len + 15u) >> 4 : len >> 4;
+    const bool fills = !PH && nch == PASS; // uniform: every chunk slot holds packet bytes
     const uint32_t lo = grp * (uint32_t)stride + 16u * gl;
     const uint32_t ustep = (uint32_t)GPW * (uint32_t)stride;
     uint32_t nbad = 0;
+    // PH: this lane's byte masks for its chunk slots (window bytes
+    // [ph + 8, ph + len) for payload_cksum, which sums from byte 8 on).
+    uint32_t msk[PH ? CPL : 1][4];
+    if constexpr (PH) {
+        const int rlo = (int)ph + (PL ? 8 : 0), rhi = (int)(ph + len);
+#pragma unroll
+        for (int c = 0; c < CPL; ++c)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                msk[c][j] = range_mask(16 * (int)(gl + (uint32_t)c * G) + 4 * j, rlo, rhi);
+    }
 
     for (uint64_t wave = xcd_block(variant) * 4u + wib; wave * PPW < n; wave += nwaves) {
         const uint64_t p0 = wave * PPW;
-        const gbyte_ptr gb = (gbyte_ptr)(base + p0 * stride);
+        const gbyte_ptr gb = (gbyte_ptr)(base - ph + p0 * stride);
         u32x4 d[U][CPL];
         if (fills && p0 + PPW <= n) { // uniform: no masks
 #pragma unroll
@@ -124,9 +153,34 @@ k_cksum_lean(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len, ui
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             uint32_t V = 0;
+            uint32_t h0 = 0, h1 = 0, h2 = 0; // packet bytes 0..11 (payload_cksum)
+            if constexpr (PH && PL) {
+                // before the masks: window dwords ph / 4 .. ph / 4 + 3 of
+                // group lanes 0 / 1, shifted to the packet start
+                uint32_t w[4];
+                using Seq = std::make_integer_sequence<int, 4>;
+                switch (ph >> 2) {
+                case 0: hdr_words_uni<G, 0>(d[u][0], w, Seq{}); break;
+                case 1: hdr_words_uni<G, 1>(d[u][0], w, Seq{}); break;
+                case 2: hdr_words_uni<G, 2>(d[u][0], w, Seq{}); break;
+                default: hdr_words_uni<G, 3>(d[u][0], w, Seq{}); break;
+                }
+                const uint32_t sh = 8u * (ph & 3u);
+                h0 = __builtin_amdgcn_alignbit(w[1], w[0], sh);
+                h1 = __builtin_amdgcn_alignbit(w[2], w[1], sh);
+                h2 = __builtin_amdgcn_alignbit(w[3], w[2], sh);
+            } else if constexpr (PL) {
+                h0 = d[u][0].x;
+                h1 = d[u][0].y;
+                h2 = d[u][0].z;
+            }
 #pragma unroll
             for (int c = 0; c < CPL; ++c) {
-                if (PL && c == 0) // payload_cksum sums from byte 8 on
+                if constexpr (PH)
+                    V = wsum4(u32x4{d[u][c].x & msk[c][0], d[u][c].y & msk[c][1],
+                                    d[u][c].z & msk[c][2], d[u][c].w & msk[c][3]},
+                              V);
+                else if (PL && c == 0) // payload_cksum sums from byte 8 on
                     V = gl == 0 ? wsum(d[u][0].w, wsum(d[u][0].z, V)) : wsum4(d[u][0], V);
                 else
                     V = wsum4(d[u][c], V);
@@ -136,9 +190,9 @@ k_cksum_lean(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len, ui
             const uint32_t v = __shfl(V, src, 64);
             Vs = mine ? v : Vs;
             if constexpr (PL) {
-                const uint32_t x = __shfl(d[u][0].x, src, 64);
-                const uint32_t y = __shfl(d[u][0].y, src, 64);
-                const uint32_t z = __shfl(d[u][0].z, src, 64);
+                const uint32_t x = __shfl(h0, src, 64);
+                const uint32_t y = __shfl(h1, src, 64);
+                const uint32_t z = __shfl(h2, src, 64);
                 hx = mine ? x : hx;
                 hy = mine ? y : hy;
                 hz = mine ? z : hz;
@@ -173,20 +227,30 @@ k_cksum_lean(const uint8_t *__restrict__ base, uint64_t stride, uint32_t len, ui
 template <int G, int CPL, int U>
 hipError_t launch_lean_shape(const LaunchArgs &a, int grid, hipStream_t st)
 {
-#define WC_LEAN_K(K, N)                                                        \
-    hipLaunchKernelGGL((k_cksum_lean<G, CPL, U, K, N>), dim3(grid), dim3(256), 0, st,   \
+    // PH: an even start phase, or a length that is not whole chunks
+    // (nontemporal loads only, the planner's default).
+    const uint32_t phase = (uint32_t)((uintptr_t)a.base & 15u);
+    const bool ph = phase != 0 || a.len % 16 != 0;
+    if (ph && (phase % 2 != 0 || a.stride % 16 != 0 || !a.nontemporal))
+        return hipErrorInvalidValue;
+#define WC_LEAN_K(K, N, P)                                                     \
+    hipLaunchKernelGGL((k_cksum_lean<G, CPL, U, K, N, P>), dim3(grid), dim3(256), 0, st, \
                        (const uint8_t *)a.base, a.stride, a.len, a.n, a.out,           \
-                       (unsigned long long *)a.bad, a.variant)
+                       (unsigned long long *)a.bad, a.variant, phase)
     if (a.kind == WC_KIND_PAYLOAD) {
-        if (a.nontemporal)
-            WC_LEAN_K(WC_KIND_PAYLOAD, true);
+        if (ph)
+            WC_LEAN_K(WC_KIND_PAYLOAD, true, true);
+        else if (a.nontemporal)
+            WC_LEAN_K(WC_KIND_PAYLOAD, true, false);
         else
-            WC_LEAN_K(WC_KIND_PAYLOAD, false);
+            WC_LEAN_K(WC_KIND_PAYLOAD, false, false);
     } else {
-        if (a.nontemporal)
-            WC_LEAN_K(WC_KIND_IP, true);
+        if (ph)
+            WC_LEAN_K(WC_KIND_IP, true, true);
+        else if (a.nontemporal)
+            WC_LEAN_K(WC_KIND_IP, true, false);
         else
-            WC_LEAN_K(WC_KIND_IP, false);
+            WC_LEAN_K(WC_KIND_IP, false, false);
     }
 #undef WC_LEAN_K
     return hipGetLastError();

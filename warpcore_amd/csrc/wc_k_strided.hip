@@ -6,18 +6,6 @@
 
 namespace wc {
 
-// payload_cksum's header window dwords K0 .. K0 + NW - 1 of a packet whose
-// start phase in its 16-byte chunk is the same for the whole batch (stride a
-// multiple of 16): window dword k is dword k & 3 of group lane k >> 2, both
-// known at compile time here, so each word is one broadcast from one lane and
-// no per-lane select.
-template <int G, int K0, int... J>
-__device__ __forceinline__ void hdr_words_uni(const u32x4 &d0, uint32_t *w,
-                                              std::integer_sequence<int, J...>)
-{
-    ((w[J] = group_bcast<G, ((K0 + J) >> 2)>(d0[(K0 + J) & 3])), ...);
-}
-
 // ---------------------------------------------------------------------------
 // Strided batches: group-per-packet kernel.
 //   G     lanes per packet (power of two, 4..64)
