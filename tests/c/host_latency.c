@@ -18,12 +18,19 @@
  *                launch
  *   floor_us     wc_cksum_strided on 1 device-resident packet + stream sync:
  *                the launch + completion floor, no PCIe data
- *   cpu1_us / cpuN_us      oracle_cksum_ragged, 1 / N threads
- *   cpu1_rx_us   oracle_rx_verdict_ragged, 1 thread
+ *   cpu1_us      oracle_cksum_ragged on the calling thread (the reference's
+ *                one engine thread)
+ *   cpuN_us      the same batch split over N threads of a PERSISTENT pool
+ *                (N - 1 workers spinning on a generation counter, plus the
+ *                caller; no thread is created per call): the box's all-core
+ *                share as a polling engine would use it
+ *   cpu1_rx_us / cpuN_rx_us   oracle_rx_verdict_ragged, 1 thread / the pool
  * Every GPU result is checked against the oracle.
  *
  *   host_latency [threads] [seconds_per_point]
  */
+#include <pthread.h>
+#include <stdatomic.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -154,9 +161,81 @@ static int c_floor(void *v)
 static int c_cpu(void *v)
 {
     struct ctx *c = v;
-    oracle_cksum_ragged(c->pool, c->off, c->len, c->n, c->out, ORACLE_KIND_IP, c->threads);
+    oracle_cksum_ragged(c->pool, c->off, c->len, c->n, c->out, ORACLE_KIND_IP, 1);
     return 0;
 }
+
+/* Persistent CPU pool: `parts` - 1 workers spin on `gen` (no sleep, no
+ * thread creation per call); a call publishes its batch, bumps gen, takes
+ * shard 0 itself and waits for the workers' `done` count. */
+static struct {
+    int parts;
+    pthread_t th[256];
+    _Atomic uint64_t gen;
+    _Atomic int done, quit;
+    struct ctx *job;
+    int rx;
+} P;
+
+static void pool_shard(int part)
+{
+    struct ctx *c = P.job;
+    const uint64_t lo = c->n * (uint64_t)part / (uint64_t)P.parts;
+    const uint64_t hi = c->n * (uint64_t)(part + 1) / (uint64_t)P.parts;
+    if (hi <= lo)
+        return;
+    if (P.rx)
+        oracle_rx_verdict_ragged(c->pool, c->off + lo, c->flen + lo, hi - lo, c->verdict + lo, 1);
+    else
+        oracle_cksum_ragged(c->pool, c->off + lo, c->len + lo, hi - lo, c->out + lo,
+                            ORACLE_KIND_IP, 1);
+}
+
+static void *pool_worker(void *arg)
+{
+    const int part = (int)(intptr_t)arg;
+    uint64_t seen = 0;
+    for (;;) {
+        uint64_t g;
+        while ((g = atomic_load_explicit(&P.gen, memory_order_acquire)) == seen)
+            if (atomic_load_explicit(&P.quit, memory_order_relaxed))
+                return NULL;
+        seen = g;
+        pool_shard(part);
+        atomic_fetch_add_explicit(&P.done, 1, memory_order_acq_rel);
+    }
+}
+
+static void pool_start(int parts)
+{
+    P.parts = parts < 1 ? 1 : parts > 256 ? 256 : parts;
+    atomic_store(&P.quit, 0);
+    atomic_store(&P.gen, 0);
+    for (int t = 1; t < P.parts; t++)
+        pthread_create(&P.th[t], NULL, pool_worker, (void *)(intptr_t)t);
+}
+
+static void pool_stop(void)
+{
+    atomic_store(&P.quit, 1);
+    for (int t = 1; t < P.parts; t++)
+        pthread_join(P.th[t], NULL);
+}
+
+static int pool_call(struct ctx *c, int rx)
+{
+    P.job = c;
+    P.rx = rx;
+    atomic_store_explicit(&P.done, 0, memory_order_relaxed);
+    atomic_fetch_add_explicit(&P.gen, 1, memory_order_release);
+    pool_shard(0);
+    while (atomic_load_explicit(&P.done, memory_order_acquire) != P.parts - 1)
+        ;
+    return 0;
+}
+
+static int c_cpu_pool(void *v) { return pool_call(v, 0); }
+static int c_cpu_pool_rx(void *v) { return pool_call(v, 1); }
 
 static int c_cpu_rx(void *v)
 {
@@ -265,24 +344,45 @@ int main(int argc, char **argv)
             }
             time_calls(c_floor, &c, secs / 2, &fl, &fl9);
             c.pool = pool;
-            c.threads = 1;
             time_calls(c_cpu, &c, secs / 2, &c1, &c19);
-            c.threads = threads;
-            time_calls(c_cpu, &c, secs / 2, &cn, &cn9);
             time_calls(c_cpu_rx, &c, secs / 2, &r1, &r19);
+            double rn, rn9;
+            pool_start(threads); /* the workers spin only while this point runs */
+            memset(out, 0, n * 2);
+            time_calls(c_cpu_pool, &c, secs / 2, &cn, &cn9);
+            if (memcmp(out, want, n * 2)) {
+                printf("host_latency: FAIL cpu pool n=%llu L=%u\n", (unsigned long long)n, L);
+                return 1;
+            }
+            memset(verdict, 0xEE, n);
+            time_calls(c_cpu_pool_rx, &c, secs / 2, &rn, &rn9);
+            pool_stop();
+            if (memcmp(verdict, vwant, n)) {
+                printf("host_latency: FAIL cpu pool rx n=%llu L=%u\n", (unsigned long long)n, L);
+                return 1;
+            }
             printf("{\"n\": %llu, \"L\": %u, \"srv_us\": %.2f, \"srv_p90_us\": %.2f, "
                    "\"zc_us\": %.2f, \"zc_p90_us\": %.2f, "
                    "\"pipe_us\": %.2f, \"rx_srv_us\": %.2f, \"rx_srv_p90_us\": %.2f, "
                    "\"rx_zc_us\": %.2f, \"rx_zc_p90_us\": %.2f, "
-                   "\"floor_us\": %.2f, \"cpu1_us\": %.3f, \"cpu%d_us\": %.2f, "
-                   "\"cpu1_rx_us\": %.3f}\n",
+                   "\"floor_us\": %.2f, \"cpu1_us\": %.3f, \"cpu%d_us\": %.3f, "
+                   "\"cpu1_rx_us\": %.3f, \"cpu%d_rx_us\": %.3f}\n",
                    (unsigned long long)n, L, sv, sv9, zc, zc9, pp, rs, rs9, rx, rx9, fl, c1,
-                   threads, cn, r1);
+                   threads, cn, r1, threads, rn);
             fflush(stdout);
         }
     }
+    uint64_t served = 0, fallbacks = 0, launches = 0;
+    wc_server_stats(&served, &fallbacks, &launches);
+    if (!served || fallbacks) {
+        /* the srv_* columns must be the server's own answers, not a fallback */
+        printf("host_latency: FAIL server answered %llu batches, %llu fell back\n",
+               (unsigned long long)served, (unsigned long long)fallbacks);
+        return 1;
+    }
     wc_host_unregister(pool);
     wc_gpu_fini();
-    printf("host_latency: ok (%s)\n", wc_version());
+    printf("host_latency: ok (%s; server answered %llu batches, 0 fallbacks, %llu grid "
+           "launches)\n", wc_version(), (unsigned long long)served, (unsigned long long)launches);
     return 0;
 }
