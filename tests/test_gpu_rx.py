@@ -37,7 +37,8 @@ def slot_ring(frames, slot: int = 2048, rng=None, pad: int = 64):
     return buf, offs, lens
 
 
-RX_MODES = {"default": {}, "plain": {"WC_RX_HDRT": "0", "WC_RX_SKIP": "0"},
+RX_MODES = {"default": {}, "ht": {"WC_RX_ADAPT": "0"},
+            "plain": {"WC_RX_HDRT": "0", "WC_RX_SKIP": "0"},
             "skip": {"WC_RX_SKIP": "1"}, "skip_plain": {"WC_RX_SKIP": "1", "WC_RX_HDRT": "0"},
             "early": {"WC_RX_EARLY": "1"},
             "early_plain": {"WC_RX_EARLY": "1", "WC_RX_HDRT": "0"},
@@ -46,10 +47,11 @@ RX_MODES = {"default": {}, "plain": {"WC_RX_HDRT": "0", "WC_RX_SKIP": "0"},
 
 @pytest.fixture(params=list(RX_MODES))
 def rx_mode(request, monkeypatch, gpu):
-    """Every kernel mode of wc_rx_verdict_* (WC_RX_EARLY: parse before or
-    during the stream; WC_RX_HDRT: header chunks loaded transposed;
-    WC_RX_SKIP: ruled-out frames leave the stream) must give the same
-    verdicts."""
+    """Every kernel mode of wc_rx_verdict_* (the default ADAPT: EARLY or the
+    HT stream per tile by the launch's running share of ruled-out frames;
+    WC_RX_EARLY: parse before or during the stream; WC_RX_HDRT: header
+    chunks loaded transposed; WC_RX_SKIP: ruled-out frames leave the stream)
+    must give the same verdicts."""
     for k, v in RX_MODES[request.param].items():
         monkeypatch.setenv(k, v)
     wc.reload_config()

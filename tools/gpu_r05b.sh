@@ -23,3 +23,14 @@ for L in 64 128 256 576; do
   done
 done
 grep -v "amdgpu.ids" $OUT/leanph.log | grep -E "^==|default|PHASE"
+# RX verdict: the ADAPT default against the fixed HT (WC_RX_ADAPT=0) and
+# EARLY modes, all-UDP and every-third-frame-ARP mixed rings, the MTU ring
+for a in 0 3; do
+  for c in zrx rx; do
+    [ $c = rx ] && [ $a = 3 ] && continue
+    echo "== $c arp=$a" >> $OUT/rxab.log
+    timeout -k 10 200 python tools/tune.py --config $c --rx-arp $a --rounds 5 --iters 20 \
+      --variants "default;WC_RX_ADAPT=0;WC_RX_EARLY=1" >> $OUT/rxab.log 2>&1 || exit 1
+  done
+done
+grep -E "^==|default|WC_RX" $OUT/rxab.log | grep -v round

@@ -115,7 +115,13 @@ struct Device {
     HostPipe pipe;
     ZeroCopy zc;
     Server srv;
+    // RX verdict ADAPT mode: one 64-bit counter per launch (seen | ruled out
+    // << 32), kRxStatSlots of them used round-robin; launch k zeroes slot
+    // k + 1 as it starts.
+    uint64_t *d_rx_stats = nullptr;
 };
+constexpr uint32_t kRxStatSlots = 1024;
+std::atomic<uint32_t> g_rx_seq{0};
 
 struct Registration {
     uint64_t bytes;
@@ -166,8 +172,14 @@ struct Config {
     int rx_early = 0;              // WC_RX_EARLY: RX verdict parses before streaming
     int rx_hdrt = 1;               // WC_RX_HDRT: RX verdict header chunks loaded transposed
     int rx_skip = 0;               // WC_RX_SKIP: frames the parse rules out leave the stream
+    int rx_adapt = 1;              // WC_RX_ADAPT: EARLY or HT per tile, by the ring's mix
     int rx_mode() const
     {
+        // The default: ADAPT (EARLY or the HT stream per tile, by the share
+        // of frames the launch's earlier tiles ruled out).  A fixed mode set
+        // by WC_RX_EARLY / WC_RX_SKIP / WC_RX_HDRT=0 / WC_RX_ADAPT=0 wins.
+        if (rx_adapt && !rx_early && !rx_skip && rx_hdrt)
+            return wc::kRxAdapt | wc::kRxHdrT;
         // EARLY streams only the frames that need the check already, so
         // SKIP has nothing to take out: it is dropped rather than sending
         // EARLY | SKIP to a variant that ignores the HDRT / NT settings.
@@ -257,6 +269,7 @@ void load_config_locked()
     c.rx_early = env_int("WC_RX_EARLY", c.rx_early);
     c.rx_hdrt = env_int("WC_RX_HDRT", c.rx_hdrt);
     c.rx_skip = env_int("WC_RX_SKIP", c.rx_skip);
+    c.rx_adapt = env_int("WC_RX_ADAPT", c.rx_adapt);
     g_cfg = c;
     g_cfg_loaded = true;
 }
@@ -321,6 +334,9 @@ int init_locked(int device, Device **out)
             return WC_ENOMEM;
         if (hipHostGetDevicePointer((void **)&D.d_stage, D.h_stage, 0) != hipSuccess ||
             hipHostGetDevicePointer((void **)&D.d_res, D.h_res, 0) != hipSuccess)
+            return WC_ENOMEM;
+        if (hipMalloc((void **)&D.d_rx_stats, kRxStatSlots * 8) != hipSuccess ||
+            hipMemset(D.d_rx_stats, 0, kRxStatSlots * 8) != hipSuccess)
             return WC_ENOMEM;
         D.ok = true;
     }
@@ -816,6 +832,17 @@ uint64_t fused_span(const uint8_t *p, uint16_t len)
 // uint8 RX verdict.
 int out_size(int kind) { return kind == kKindRx ? 1 : 2; }
 
+// One RX verdict launch with this launch's ADAPT counter slot.
+hipError_t rx_launch(const Device &D, const Config &C, const void *base, const uint64_t *offs,
+                     const uint16_t *flens, uint64_t n, uint8_t *verdict, uint64_t *drops,
+                     hipStream_t st)
+{
+    const uint32_t k = g_rx_seq.fetch_add(1) % kRxStatSlots;
+    return wc::launch_rx_verdict(base, offs, flens, n, verdict, drops, C.nt != 0, st,
+                                 C.rx_mode(), D.d_rx_stats + k,
+                                 D.d_rx_stats + (k + 1) % kRxStatSlots);
+}
+
 // One device launch over a ragged batch of `kind` (a checksum kind, RX
 // verdicts -- lengths are frame lengths --, or the fused pair, whose header
 // checksums go to d_out_hdr).
@@ -824,8 +851,7 @@ int run_ragged_any(const Device &D, const Config &C, const uint8_t *d_base, cons
                    hipStream_t st, uint16_t *d_out_hdr = nullptr)
 {
     if (kind == kKindRx)
-        return hip_err(wc::launch_rx_verdict(d_base, d_off, d_len, n, (uint8_t *)d_out, nullptr,
-                                             C.nt != 0, st, C.rx_mode()));
+        return hip_err(rx_launch(D, C, d_base, d_off, d_len, n, (uint8_t *)d_out, nullptr, st));
     const bool fused = kind == kKindFused;
     const int k = fused ? WC_CKSUM_PAYLOAD : kind;
     const Plan p = plan_ragged(D, C, n, k, zero_copy, fused);
@@ -1670,8 +1696,8 @@ int wc_rx_verdict_ragged(const void *d_base, const uint64_t *d_off, const uint16
     int rc = ensure_device(&D, &C);
     if (rc)
         return rc;
-    return hip_err(wc::launch_rx_verdict(d_base, d_off, d_frame_len, n, d_verdict, d_drops,
-                                         C.nt != 0, (hipStream_t)stream, C.rx_mode()));
+    return hip_err(rx_launch(*D, C, d_base, d_off, d_frame_len, n, d_verdict, d_drops,
+                             (hipStream_t)stream));
 }
 
 int wc_rx_verdict_host(const void *h_base, uint64_t h_bytes, const uint64_t *h_off,
@@ -1936,6 +1962,8 @@ int wc_gpu_fini(void)
             (void)hipHostFree(D.srv.h_hb);
         }
         (void)hipStreamSynchronize(D.scalar_st);
+        (void)hipDeviceSynchronize(); // (an RX launch may still use d_rx_stats)
+        (void)hipFree(D.d_rx_stats);
         (void)hipStreamDestroy(D.scalar_st);
         (void)hipHostFree(D.h_stage);
         (void)hipHostFree(D.h_res);
