@@ -1,5 +1,5 @@
 /*
- * tx_queue_loop.c -- the TX batch hook of INTEGRATION.md section 2, compiled
+ * tx_queue_loop.c -- the TX batch hook of INTEGRATION.md section 3, compiled
  * and driven the way the reference sends a w_iov_sq.
  *
  * The reference's w_tx walks the queue iov by iov and calls udp_tx on each

@@ -191,7 +191,7 @@ def test_c_host_latency_tool(gpu, tmp_path):
 
 
 def test_c_tx_queue_loop(gpu, tmp_path):
-    """INTEGRATION.md section 2's TX hook compiled in C and driven like w_tx
+    """INTEGRATION.md section 3's TX hook compiled in C and driven like w_tx
     (backend_netmap.c:348-358): per w_iov_sq, headers built as mk_ip4_hdr /
     mk_ip6_hdr / udp_tx do, ONE wc_cksum_ip_udp_host call, both results
     stored raw (zero-checksum sockets keep udp->cksum 0), the TX-ring-full
