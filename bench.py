@@ -105,6 +105,10 @@ def parse(argv=None):
     ap.add_argument("--graph", default="auto", choices=["auto", "on", "off"],
                     help="replay the timed launches from a captured hipGraph (auto: for c3, "
                          "where a Python launch can take longer than the kernel)")
+    ap.add_argument("--rx-arp", type=int, default=0,
+                    help="rx / zrx: every K-th frame an ARP frame (needs no UDP check)")
+    ap.add_argument("--no-rings", action="store_true",
+                    help="skip the netmap RX-ring legs (rx, zrx, zrx with ARP) of the default line")
     ap.add_argument("--c3-packets", type=int, default=1 << 20, help="packets per c3 size")
     ap.add_argument("--c4-packets", type=int, default=1 << 24, help="packets of the c4 object")
     ap.add_argument("--extra-seconds", type=float, default=0.25,
@@ -245,6 +249,10 @@ def make_workload(args, dev, rank, world):
         buf = torch.empty(n * slot + 64, dtype=torch.uint8, device=dev)
         wc.synth_fill(buf, seed, nbytes=n * slot)
         f_off, f_len = synth.make_rx_ring(buf, n, ip_lens, slot=slot)
+        if args.rx_arp:  # every K-th frame ARP: its EtherType rules it out (eth.c:75-86)
+            sel = torch.from_numpy(f_off[::args.rx_arp].astype(np.int64)).to(dev)
+            buf[sel + 12] = 0x08
+            buf[sel + 13] = 0x06
         d_off = torch.from_numpy(f_off).to(dev)
         d_len = torch.from_numpy(f_len).to(dev)
         out = torch.empty(n, dtype=torch.uint8, device=dev)
@@ -260,6 +268,9 @@ def make_workload(args, dev, rank, world):
                 f"checksums, ip4_rx + udp_rx checks) per frame")
         meta = {"packets_per_gpu": n, "mean_frame_bytes": round(nbytes / n, 2), "slot_bytes": slot,
                 "layout": "ragged", "kind": "rx_verdict"}
+        if args.rx_arp:
+            meta["arp_every"] = args.rx_arp
+            desc += f"; every {args.rx_arp}th frame ARP (no UDP check)"
         if args.config == "rx":
             meta["packet_bytes"] = args.len + 42  # frame: Ethernet 14 + IP/UDP 28 + payload
         plan = {"kernel": "k_rx_verdict (header parse + gathered seg stream)",
@@ -769,7 +780,19 @@ def extra_legs(args, dev, rank, world, coll_dev):
     c4 = measure_leg(args, dev, rank, world, coll_dev, sub, use_graph=True)
     c4["workload"] = (f"BASELINE configs[3]: {args.c4_packets} packets, Zipf(s=1) lengths "
                       f"64-1472 B, packed (unaligned starts), ip_cksum")
-    return c2rot, c3, c4
+    rings = None
+    if not args.no_rings:
+        # the RX verdict over netmap RX rings (device-resident),
+        # beside the headline: MTU frames, C4's Zipf sizes, and the Zipf ring
+        # with every third frame ARP (the default ADAPT mode's other case)
+        rings = {"workload": ("netmap RX rings, one frame per 2048-B slot, the RX verdict "
+                              "(wc_rx_verdict_ragged) of every frame; bytes = frame bytes; "
+                              "every verdict checked against oracle_rx_verdict")}
+        for name, cfg, arp in (("rx_mtu", "rx", 0), ("zrx", "zrx", 0), ("zrx_arp3", "zrx", 3)):
+            sub = copy.copy(base)
+            sub.config, sub.packets, sub.len, sub.rx_arp = cfg, 1 << 20, 1472, arp
+            rings[name] = measure_leg(args, dev, rank, world, coll_dev, sub, use_graph=False)
+    return c2rot, c3, c4, rings
 
 
 def main():
@@ -867,9 +890,9 @@ def main():
     del T, W, out
     torch.cuda.synchronize(dev)
     torch.cuda.empty_cache()
-    c2rot = c3 = c4 = None
+    c2rot = c3 = c4 = rings = None
     if not args.no_extra and args.config == "c2" and not args.fused and args.kind == "ip":
-        c2rot, c3, c4 = extra_legs(args, dev, rank, world, coll_dev)
+        c2rot, c3, c4, rings = extra_legs(args, dev, rank, world, coll_dev)
     c5 = None
     if not args.no_c5 and args.config != "c5":
         c5 = c5_leg(args, dev, rank, world, coll_dev)
@@ -915,6 +938,8 @@ def main():
         if c3 is not None:
             line["c3"] = c3
             line["c4"] = c4
+        if rings is not None:
+            line["rings"] = rings
         if gather is not None:
             line["results_allgather"] = gather
         print(json.dumps(line), flush=True)
