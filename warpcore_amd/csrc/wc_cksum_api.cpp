@@ -698,9 +698,12 @@ uint16_t scalar_cksum(const void *buf, uint16_t len, int kind, const char *who)
     const size_t span =
         kind == WC_CKSUM_PAYLOAD ? std::max<size_t>(len, 20) : (size_t)len;
     memcpy(D->h_stage, buf, span);
+    // (the load flavour the planner assumed: the lean kernel's phase path,
+    // which a 1-packet batch at an even staging phase may take, exists with
+    // nontemporal loads only)
     Plan p = plan_strided(*D, g_cfg, (uint64_t)D->d_stage, 0, len, 1, kind);
     wc::LaunchArgs a{D->d_stage, 0,   len,  nullptr, nullptr, 1,
-                     D->d_res,   nullptr, kind, false,   p.full,  false};
+                     D->d_res,   nullptr, kind, false,   p.full,  g_cfg.nt != 0};
     rc = run(*D, g_cfg, a, p, D->scalar_st);
     if (rc)
         die(who, rc);
