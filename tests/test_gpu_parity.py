@@ -475,11 +475,15 @@ def test_lean_phase_slots(gpu, monkeypatch, length, lean_phase):
                 b[o] = 0x4F
             elif k == 1:
                 b[o] = 0x41
-            elif k == 2:
+            elif k == 2 and length >= 40:
                 b[o] = 0x60
-                if length > 6:
-                    b[o + 6] = 254 + (i & 1)
-            elif k == 3:
+                b[o + 6] = 254 + (i & 1)
+            elif k == 3 or (k == 2 and length < 40):
+                b[o] = 0x45
+            elif ((b[o] & 15) * 4 if (b[o] >> 4) == 4 else 40) > length:
+                # a random header longer than the packet (any version but 4
+                # is IPv6's 40 bytes): payload_cksum of len < hl reads ~4 GiB
+                # in the reference (undefined there)
                 b[o] = 0x45
         d = dev_u8(b, gpu)
         for kind, kn in (("ip", 0), ("payload", 1)):
