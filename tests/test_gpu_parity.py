@@ -493,7 +493,8 @@ def test_lean_phase_slots(gpu, monkeypatch, length, lean_phase):
             want = c_oracle.cksum_strided(b, stride, length, n, kind=kn, byte_offset=start)
             np.testing.assert_array_equal(got, want, err_msg=f"{kind} start {start}")
     plan = wc.plan_strided(0x100000000 + 14, stride, length, n, kind="ip")
-    assert (plan["kernel"] == "lean") == (lean_phase == "1" and length <= 48 * 16 - 14 - 15)
+    # lean up to WC_LEAN_MAX = 48 chunks of the window at phase 14
+    assert (plan["kernel"] == "lean") == (lean_phase == "1" and (14 + length + 15) // 16 <= 48)
 
 
 @pytest.mark.parametrize("length", [60, 64, 100, 333, 1000, 1500])
