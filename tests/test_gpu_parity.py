@@ -492,9 +492,13 @@ def test_lean_phase_slots(gpu, monkeypatch, length, lean_phase):
             got = host(wc.cksum_strided(d, stride, length, n, kind=kind, byte_offset=start))
             want = c_oracle.cksum_strided(b, stride, length, n, kind=kn, byte_offset=start)
             np.testing.assert_array_equal(got, want, err_msg=f"{kind} start {start}")
-    plan = wc.plan_strided(0x100000000 + 14, stride, length, n, kind="ip")
-    # lean up to WC_LEAN_MAX = 48 chunks of the window at phase 14
-    assert (plan["kernel"] == "lean") == (lean_phase == "1" and (14 + length + 15) // 16 <= 48)
+    # the phase path is planned for payload_cksum of 48 B up to 18 window
+    # chunks at phase 14 (where it measured faster than the group kernel)
+    for kind in ("ip", "payload"):
+        plan = wc.plan_strided(0x100000000 + 14, stride, length, n, kind=kind)
+        want = (lean_phase == "1" and kind == "payload" and length >= 48
+                and (14 + length + 15) // 16 <= 18)
+        assert (plan["kernel"] == "lean") == want, (kind, plan)
 
 
 @pytest.mark.parametrize("length", [60, 64, 100, 333, 1000, 1500])

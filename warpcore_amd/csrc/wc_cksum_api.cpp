@@ -115,13 +115,16 @@ struct Device {
     HostPipe pipe;
     ZeroCopy zc;
     Server srv;
-    // RX verdict ADAPT mode: one 64-bit counter per launch (seen | ruled out
-    // << 32), kRxStatSlots of them used round-robin; launch k zeroes slot
-    // k + 1 as it starts.
-    uint64_t *d_rx_stats = nullptr;
+    // RX verdict ADAPT mode: kRxSets tally arrays in mapped pinned memory,
+    // one per recent launch (launch g writes set g % kRxSets), and the mode
+    // the newest tally chose (rx_launch).
+    uint32_t *h_rx_tally[4] = {}, *d_rx_tally[4] = {};
+    uint32_t rx_words[4] = {}; // tally words launch g % kRxSets may write
+    uint32_t rx_gen = 0;
+    bool rx_early = false;
 };
-constexpr uint32_t kRxStatSlots = 1024;
-std::atomic<uint32_t> g_rx_seq{0};
+constexpr int kRxSets = 4;
+std::mutex g_rx_mu; // rx_launch's tally bookkeeping (batch calls run outside g_mu)
 
 struct Registration {
     uint64_t bytes;
@@ -335,9 +338,14 @@ int init_locked(int device, Device **out)
         if (hipHostGetDevicePointer((void **)&D.d_stage, D.h_stage, 0) != hipSuccess ||
             hipHostGetDevicePointer((void **)&D.d_res, D.h_res, 0) != hipSuccess)
             return WC_ENOMEM;
-        if (hipMalloc((void **)&D.d_rx_stats, kRxStatSlots * 8) != hipSuccess ||
-            hipMemset(D.d_rx_stats, 0, kRxStatSlots * 8) != hipSuccess)
-            return WC_ENOMEM;
+        for (int k = 0; k < kRxSets; ++k) {
+            if (hipHostMalloc((void **)&D.h_rx_tally[k], wc::kRxTallyWords * 4,
+                              hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+                hipHostGetDevicePointer((void **)&D.d_rx_tally[k], D.h_rx_tally[k], 0) !=
+                    hipSuccess)
+                return WC_ENOMEM;
+            memset(D.h_rx_tally[k], 0, wc::kRxTallyWords * 4);
+        }
         D.ok = true;
     }
     *out = &D;
@@ -563,10 +571,16 @@ Plan plan_strided(const Device &D, const Config &C, uint64_t base, uint64_t stri
     // first lane.  payload_cksum needs len >= 48 there (the whole IPv4 /
     // IPv6 header inside the packet); up to WC_LEAN_MAX chunks.
     const bool aligned16 = base % 16 == 0 && stride % 16 == 0 && len % 16 == 0 && len != 0;
-    // Sparse packets at one even start phase (netmap slots: IP packets at
-    // +14) take it too, with per-slot byte masks (PH, wc_k_lean.hip).
+    // Sparse payload_cksum packets at one even start phase (netmap slots: IP
+    // packets at +14) of up to 18 window chunks take it too, with per-slot
+    // byte masks (PH, wc_k_lean.hip): in 2048-B slots at +14, from HBM,
+    // payload 64 B 24.2 -> 22.5 us, 128 B 41.3 -> 39.8, 256 B 58.2 -> 56.1
+    // against the group kernel, within 1 us of ip_cksum; ip_cksum gains
+    // nothing (128 B 39.2 -> 41.2 us) and 576 B loses on both kinds (96.9 ->
+    // 112.7 us), so they keep the group kernel (profiles/ab_r05_lean_phase.log).
     const bool phased = !aligned16 && C.lean_phase && C.nt && stride % 16 == 0 &&
-                        base % 2 == 0 && len != 0 && !packed && sseg != 2;
+                        base % 2 == 0 && len != 0 && !packed && sseg != 2 && payload &&
+                        nch <= 18;
     if (!hdr && C.lean_max > 0 && (aligned16 || phased) && (!payload || len >= 48) &&
         nch <= (uint32_t)C.lean_max && (sseg != 2 || !packed)) {
         const wc::Shape sh = C.have_shape ? C.shape : aligned16 ? lean_shape_for(nch)
@@ -835,21 +849,53 @@ uint64_t fused_span(const uint8_t *p, uint16_t len)
 // uint8 RX verdict.
 int out_size(int kind) { return kind == kKindRx ? 1 : 2; }
 
-// One RX verdict launch with this launch's ADAPT counter slot.
-hipError_t rx_launch(const Device &D, const Config &C, const void *base, const uint64_t *offs,
+// One RX verdict launch.  ADAPT (the default): EARLY or HT by the newest
+// earlier launch on this device whose tally has arrived (>= 8 sampled tiles,
+// or all it will write): EARLY when more than 1 in 8 of its sampled frames
+// needed no UDP check (ARP / ICMP / TCP / zero checksums / drops), else HT;
+// the previous choice stands until a tally arrives.  The kernel's tally is a
+// store per 64 tiles into mapped host memory -- nothing to wait for here,
+// and launches stay asynchronous (a tally read while its launch still runs
+// is a partial sample).
+hipError_t rx_launch(Device &D, const Config &C, const void *base, const uint64_t *offs,
                      const uint16_t *flens, uint64_t n, uint8_t *verdict, uint64_t *drops,
                      hipStream_t st)
 {
-    const uint32_t k = g_rx_seq.fetch_add(1) % kRxStatSlots;
-    return wc::launch_rx_verdict(base, offs, flens, n, verdict, drops, C.nt != 0, st,
-                                 C.rx_mode(), D.d_rx_stats + k,
-                                 D.d_rx_stats + (k + 1) % kRxStatSlots);
+    const int mode = C.rx_mode();
+    if (!(mode & wc::kRxAdapt) || !D.h_rx_tally[0])
+        return wc::launch_rx_verdict(base, offs, flens, n, verdict, drops, C.nt != 0, st, mode);
+    std::lock_guard<std::mutex> lk(g_rx_mu);
+    for (uint32_t back = 1; back < (uint32_t)kRxSets && back <= D.rx_gen; ++back) {
+        const uint32_t g = D.rx_gen - back;
+        const int set = (int)(g % kRxSets);
+        const volatile uint32_t *t = D.h_rx_tally[set];
+        uint32_t words = 0, seen = 0, out = 0;
+        for (uint32_t i = 0; i < D.rx_words[set]; ++i) {
+            const uint32_t w = t[i];
+            if ((w >> 16) != (g & 0xFFFFu))
+                continue;
+            ++words;
+            seen += w & 0xFFu;
+            out += (w >> 8) & 0xFFu;
+        }
+        if (words >= 8 || (words && words == D.rx_words[set])) {
+            D.rx_early = out * 8u > seen;
+            break;
+        }
+    }
+    const uint32_t g = ++D.rx_gen;
+    const int set = (int)(g % kRxSets);
+    const uint64_t tiles = (n + 63) / 64;
+    D.rx_words[set] = (uint32_t)std::min<uint64_t>((tiles + 63) / 64, wc::kRxTallyWords);
+    const int m = wc::kRxHdrT | (D.rx_early ? wc::kRxEarly : 0);
+    return wc::launch_rx_verdict(base, offs, flens, n, verdict, drops, C.nt != 0, st, m,
+                                 D.d_rx_tally[set], g & 0xFFFFu);
 }
 
 // One device launch over a ragged batch of `kind` (a checksum kind, RX
 // verdicts -- lengths are frame lengths --, or the fused pair, whose header
 // checksums go to d_out_hdr).
-int run_ragged_any(const Device &D, const Config &C, const uint8_t *d_base, const uint64_t *d_off,
+int run_ragged_any(Device &D, const Config &C, const uint8_t *d_base, const uint64_t *d_off,
                    const uint16_t *d_len, uint64_t n, void *d_out, int kind, bool zero_copy,
                    hipStream_t st, uint16_t *d_out_hdr = nullptr)
 {
@@ -1965,8 +2011,9 @@ int wc_gpu_fini(void)
             (void)hipHostFree(D.srv.h_hb);
         }
         (void)hipStreamSynchronize(D.scalar_st);
-        (void)hipDeviceSynchronize(); // (an RX launch may still use d_rx_stats)
-        (void)hipFree(D.d_rx_stats);
+        (void)hipDeviceSynchronize(); // (an RX launch may still write its tally)
+        for (int k = 0; k < kRxSets; ++k)
+            (void)hipHostFree(D.h_rx_tally[k]);
         (void)hipStreamDestroy(D.scalar_st);
         (void)hipHostFree(D.h_stage);
         (void)hipHostFree(D.h_res);

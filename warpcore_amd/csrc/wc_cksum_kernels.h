@@ -167,15 +167,16 @@ hipError_t launch_synth(void *buf, uint64_t nbytes, uint64_t seed, int grid,
 // drops (optional) accumulates the frames the reference's RX path drops.
 // mode: kRxEarly (parse, then stream only the checked frames) | kRxHdrT
 // (transposed header loads) | kRxSkip (frames the parse rules out leave the
-// stream) | kRxAdapt (EARLY or the HT stream per tile, by the share of frames
-// the launch's earlier tiles ruled out; needs `stats`, this launch's zeroed
-// counter, and `stats_next`, the next launch's, which it zeroes); every mode
-// gives the same verdicts.
+// stream); every mode gives the same verdicts.  `tally` (mapped host memory,
+// kRxTallyWords words; ADAPT, with HT and without SKIP): every 64th tile
+// stores gen << 16 | frames ruled out << 8 | frames, for the host's choice
+// of EARLY or HT for the next launch.
 constexpr int kRxEarly = 2, kRxHdrT = 4, kRxSkip = 8, kRxAdapt = 16;
+constexpr uint32_t kRxTallyWords = 1024;
 hipError_t launch_rx_verdict(const void *base, const uint64_t *offs, const uint16_t *flens,
                              uint64_t n, uint8_t *verdict, uint64_t *drops, bool nt,
-                             hipStream_t st, int mode = 0, uint64_t *stats = nullptr,
-                             uint64_t *stats_next = nullptr);
+                             hipStream_t st, int mode = 0, uint32_t *tally = nullptr,
+                             uint32_t gen = 0);
 
 // Resident small-batch server (wc_k_serve.hip).  Host-mapped pinned memory:
 // one record per packet, written by the host (seq last), polled / read by the

@@ -282,27 +282,25 @@ __device__ __forceinline__ RxParse rx_parse_slow(uint64_t fa, uint32_t flen, boo
 //   HT     the header chunks are loaded transposed (rx_load_t);
 //   SKIP   (with !EARLY) once parsed, frames that need no check leave the
 //          stream: its later row groups read the zero chunk for them.
-//   ADAPT  (the default) each tile takes EARLY or the HT stream by what the
-//          launch's earlier tiles saw: every 8th tile adds its frame count and
-//          the count of frames that needed no UDP check (not IP, not UDP,
-//          zero checksum, drops) to one 64-bit counter of this launch
-//          (`stats`: seen | ruled out << 32); a tile starts by reading it and
-//          parses first (EARLY) once at least 512 frames were seen and more
-//          than 1 in 8 of them were ruled out.  An all-UDP ring stays on the
-//          HT stream, a ring with much ARP / ICMP / TCP moves to EARLY after
-//          its first tiles.  The counter of the next launch (stats_next) is
-//          zeroed by this launch's first wave.
+//   TALLY  (with the default ADAPT mode, wc_cksum_api.cpp rx_launch) every
+//          64th tile writes how many of its frames needed no UDP check (not
+//          IP, not UDP, zero checksum, drops) and how many it held, one word
+//          per tile `tally[tile / 64] = gen << 16 | ruled_out << 8 | frames`,
+//          with a plain store into mapped host memory; the host picks EARLY
+//          or HT for the device's next launch from the newest complete
+//          tally.  No load and no atomic in the kernel: a first version kept
+//          one device counter per launch that every tile read and every 8th
+//          tile added to, and the same-address atomics serialised the mixed
+//          ring from 113 to 458 us (profiles/ab_r05_rx_adapt.log).
 // (4 waves per SIMD for every mode: capping the EARLY kernels at 96 VGPRs
 // for 5 spilled 4 of them and took the mixed ring from 114 to 141 us,
 // profiles/ab_r04_rx_early_waves.log.)
-template <bool NT, bool EARLY, bool HT, bool SKIP, bool ADAPT = false>
+template <bool NT, bool EARLY, bool HT, bool SKIP, bool TALLY = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
 k_rx_verdict(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
              const uint16_t *__restrict__ flens, uint64_t n, uint8_t *__restrict__ verdict,
-             unsigned long long *__restrict__ drops, unsigned long long *__restrict__ stats,
-             unsigned long long *__restrict__ stats_next)
+             unsigned long long *__restrict__ drops, uint32_t *__restrict__ tally, uint32_t gen)
 {
-    static_assert(!ADAPT || (!EARLY && !SKIP), "ADAPT picks EARLY per tile, without SKIP");
     constexpr int UNS = 4;
     using Src = GathSrc<UNS, NT, SKIP && !EARLY>;
     struct Lds {
@@ -325,12 +323,6 @@ k_rx_verdict(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
     uint64_t off_n;
     uint32_t flen_n;
     meta_load(offs, flens, tile * 64 + lane, n, off_n, flen_n);
-    uint64_t seen_out = 0; // ADAPT: this launch's counter as the wave starts
-    if constexpr (ADAPT) {
-        seen_out = __hip_atomic_load(stats, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (blockIdx.x == 0 && threadIdx.x == 0)
-            __hip_atomic_store(stats_next, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
 
     for (; tile < ntiles; tile += nwaves) {
         const uint64_t p = tile * 64 + lane;
@@ -353,14 +345,7 @@ k_rx_verdict(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
         bool slow = false;
         RxParse h{};
         uint32_t v;
-        bool early = EARLY;
-        if constexpr (ADAPT) {
-            const uint32_t seen = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)seen_out);
-            const uint32_t out =
-                (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(seen_out >> 32));
-            early = seen >= 512u && out * 8u > seen;
-        }
-        if (early) {
+        if constexpr (EARLY) {
             headers();
             h = rx_parse(c, fa, flen, valid, slow);
             v = h.verdict;
@@ -420,14 +405,13 @@ k_rx_verdict(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
                 v = h.verdict;
             }
         }
-        if constexpr (ADAPT) {
-            if ((tile & 7u) == 0) { // this tile's share of the launch's statistics
+        if constexpr (TALLY) {
+            if ((tile & 63u) == 0 && (tile >> 6) < kRxTallyWords) { // a sample of the mix
                 const uint32_t nv = __builtin_popcountll(__ballot(valid));
                 const uint32_t nout = __builtin_popcountll(__ballot(valid && !h.need));
                 if (lane == 0)
-                    __hip_atomic_fetch_add(stats, (unsigned long long)nv |
-                                                      ((unsigned long long)nout << 32),
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store(&tally[tile >> 6], (gen << 16) | (nout << 8) | nv,
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             }
         }
         if (__ballot(slow)) { // IPv4 headers with more than 20 B of options, IHL < 5
@@ -451,41 +435,45 @@ k_rx_verdict(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
 
 } // namespace
 
-template <bool NT, bool EARLY, bool HT, bool SKIP, bool ADAPT = false>
+template <bool NT, bool EARLY, bool HT, bool SKIP, bool TALLY = false>
 static hipError_t launch_rx_one(const void *base, const uint64_t *offs, const uint16_t *flens,
                                 uint64_t n, uint8_t *verdict, uint64_t *drops, int grid,
-                                hipStream_t st, uint64_t *stats, uint64_t *stats_next)
+                                hipStream_t st, uint32_t *tally, uint32_t gen)
 {
-    hipLaunchKernelGGL((k_rx_verdict<NT, EARLY, HT, SKIP, ADAPT>), dim3(grid), dim3(256), 0, st,
+    hipLaunchKernelGGL((k_rx_verdict<NT, EARLY, HT, SKIP, TALLY>), dim3(grid), dim3(256), 0, st,
                        (const uint8_t *)base, offs, flens, n, verdict,
-                       (unsigned long long *)drops, (unsigned long long *)stats,
-                       (unsigned long long *)stats_next);
+                       (unsigned long long *)drops, tally, gen);
     return hipGetLastError();
 }
 
 hipError_t launch_rx_verdict(const void *base, const uint64_t *offs, const uint16_t *flens,
                              uint64_t n, uint8_t *verdict, uint64_t *drops, bool nt,
-                             hipStream_t st, int mode, uint64_t *stats, uint64_t *stats_next)
+                             hipStream_t st, int mode, uint32_t *tally, uint32_t gen)
 {
     const uint64_t tiles = (n + 63) / 64;
     const int grid = (int)std::min<uint64_t>(
         kMaxGridBlocks, std::max<uint64_t>(1, (tiles + kFlatWaves - 1) / kFlatWaves));
     // EARLY streams only the checked frames: SKIP has nothing to skip there,
-    // and is dropped so that NT and HDRT are still honoured.  ADAPT (with
-    // its counters) picks EARLY or the HT stream per tile; it overrides both.
-    if ((mode & kRxAdapt) && stats && stats_next) {
-        if (nt)
-            return launch_rx_one<true, false, true, false, true>(base, offs, flens, n, verdict,
-                                                                 drops, grid, st, stats,
-                                                                 stats_next);
-        return launch_rx_one<false, false, true, false, true>(base, offs, flens, n, verdict,
-                                                              drops, grid, st, stats, stats_next);
-    }
+    // and is dropped so that NT and HDRT are still honoured.
     const bool early = mode & kRxEarly, ht = mode & kRxHdrT, skip = (mode & kRxSkip) && !early;
+    if (tally && !skip && ht) { // ADAPT: the host chose EARLY or HT; the kernel tallies
+        if (nt)
+            return early ? launch_rx_one<true, true, true, false, true>(base, offs, flens, n,
+                                                                        verdict, drops, grid,
+                                                                        st, tally, gen)
+                         : launch_rx_one<true, false, true, false, true>(base, offs, flens, n,
+                                                                         verdict, drops, grid,
+                                                                         st, tally, gen);
+        return early ? launch_rx_one<false, true, true, false, true>(base, offs, flens, n, verdict,
+                                                                     drops, grid, st, tally, gen)
+                     : launch_rx_one<false, false, true, false, true>(base, offs, flens, n,
+                                                                      verdict, drops, grid, st,
+                                                                      tally, gen);
+    }
 #define WC_RX(N, E, H, S)                                                      \
     if (nt == N && early == E && ht == H && skip == S)                         \
         return launch_rx_one<N, E, H, S>(base, offs, flens, n, verdict, drops, grid, st,   \
-                                         nullptr, nullptr);
+                                         nullptr, 0u);
 #define WC_RX_NT(N)                                                            \
     WC_RX(N, false, false, false) WC_RX(N, false, false, true)                 \
     WC_RX(N, false, true, false) WC_RX(N, false, true, true)                   \
