@@ -501,6 +501,48 @@ def test_lean_phase_slots(gpu, monkeypatch, length, lean_phase):
         assert (plan["kernel"] == "lean") == want, (kind, plan)
 
 
+@pytest.mark.parametrize("piece", [1, 777, 4096])
+def test_split_launches(gpu, monkeypatch, piece):
+    """WC_SPLIT_PKTS: a batch larger than the piece runs as back-to-back
+    launches of `piece` packets (each piece planned on its own: its base, its
+    phase) -- strided (C2-shaped, netmap slots at +14, packed at odd offsets),
+    ragged (Zipf, packed), fused, and the verify count, all equal to the
+    oracle / to one launch."""
+    monkeypatch.setenv("WC_SPLIT_PKTS", str(piece))
+    wc.reload_config()
+    try:
+        rng = np.random.default_rng(piece)
+        n = 10000
+        for L, stride, at, kind in ((1472, 1472, 0, "ip"), (300, 2048, 14, "payload"),
+                                    (200, 201, 3, "ip"), (1500, 1500, 7, "payload")):
+            buf = rng.integers(0, 256, at + n * stride + 64, dtype=np.uint8)
+            got = host(wc.cksum_strided(dev_u8(buf, gpu), stride, L, n, kind=kind,
+                                        byte_offset=at))
+            want = c_oracle.cksum_strided(buf, stride, L, n, kind=0 if kind == "ip" else 1,
+                                          byte_offset=at)
+            np.testing.assert_array_equal(got, want, err_msg=f"{L} {stride} +{at} {kind}")
+        lens = synth.zipf_lengths(n, seed=piece)
+        offs = synth.packed_offsets(lens, lead=5)
+        buf = rng.integers(0, 256, int(offs[-1]) + int(lens[-1]) + 64, dtype=np.uint8)
+        d = dev_u8(buf, gpu)
+        d_off = torch.from_numpy(offs.astype(np.int64)).to(gpu)
+        d_len = torch.from_numpy(lens.astype(np.int16)).to(gpu)
+        for kind, k in (("ip", 0), ("payload", 1)):
+            got = host(wc.cksum_ragged(d, d_off, d_len, kind=kind))
+            np.testing.assert_array_equal(got, c_oracle.cksum_ragged(buf, offs, lens, kind=k))
+        synth.stamp_udp_headers(d, d_off, d_len)
+        buf = host(d)[: buf.size].view(np.uint8)
+        hdr, pay = wc.cksum_ip_udp_ragged(d, d_off, d_len)
+        want_h, want_p = fused_want(buf, offs, lens)
+        np.testing.assert_array_equal(host(hdr), want_h)
+        np.testing.assert_array_equal(host(pay), want_p)
+        out, bad = wc.verify_ragged(d, d_off, d_len, kind="payload")
+        assert int(bad.item()) == int((want_p != 0).sum())
+    finally:
+        monkeypatch.delenv("WC_SPLIT_PKTS")
+        wc.reload_config()
+
+
 @pytest.mark.parametrize("length", [60, 64, 100, 333, 1000, 1500])
 def test_strided_packed_seg_wild_payload(gpu, monkeypatch, length):
     """payload_cksum on the seg-only packed strided kernel with random header

@@ -4,7 +4,7 @@
 # 16-thread CPU pool (profiles/host_latency_r05.log).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=gpurun_out/r05c
+OUT=gpurun_out/${R05C_OUT:-r05c}
 mkdir -p $OUT
 export TMPDIR=/tmp WC_NO_BUILD=1
 timeout -k 10 300 python -u tools/serve_interference.py --rounds 5 > $OUT/serve_interference.log 2>&1

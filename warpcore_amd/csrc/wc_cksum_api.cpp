@@ -163,6 +163,7 @@ struct Config {
     int flat_pk = 1;               // WC_FLAT_PK: flat kernel chunks per lane slot
     int gather = 1;                // WC_GATHER: seg kernel's gathered-stream path (0 off, 2 forced)
     int lean_max = 48;             // WC_LEAN_MAX: lean kernel for aligned packets up to this many chunks
+    uint64_t split_pkts = 0;       // WC_SPLIT_PKTS: batches above this many packets run as back-to-back launches of it
     int lean_phase = 1;            // WC_LEAN_PHASE: lean kernel for sparse packets at an even phase too
     int serve = 1;                 // WC_SERVE: resident server for small registered host batches
     int serve_waves = 64;          // WC_SERVE_WAVES: its waves (one 64-lane workgroup each)
@@ -264,6 +265,7 @@ void load_config_locked()
     c.flat_pk = env_int("WC_FLAT_PK", c.flat_pk);
     c.gather = env_int("WC_GATHER", c.gather);
     c.lean_max = env_int("WC_LEAN_MAX", c.lean_max);
+    c.split_pkts = env_u64("WC_SPLIT_PKTS", c.split_pkts);
     c.lean_phase = env_int("WC_LEAN_PHASE", c.lean_phase);
     c.serve = env_int("WC_SERVE", c.serve);
     c.serve_waves = std::max(1, std::min(env_int("WC_SERVE_WAVES", c.serve_waves), 1024));
@@ -662,13 +664,22 @@ int batch_strided(const void *d_base, uint64_t stride, uint16_t len, uint64_t n,
     int rc = ensure_device(&D, &C);
     if (rc)
         return rc;
-    const Plan p =
-        plan_strided(*D, C, (uint64_t)d_base, stride, len, n, kind, d_out_hdr != nullptr);
-    wc::LaunchArgs a{d_base, stride, len,  nullptr,  nullptr, n,
-                     d_out,  d_bad,  kind, false,    p.full,  C.nt != 0,
-                     0,      d_out_hdr};
-    a.variant = C.variant;
-    return run(*D, C, a, p, (hipStream_t)stream);
+    // A batch larger than C.split_pkts runs as back-to-back launches of that
+    // many packets on the same stream (WC_SPLIT_PKTS; 0 = one launch).
+    const uint64_t piece = C.split_pkts && n > C.split_pkts && stride ? C.split_pkts : n;
+    for (uint64_t p0 = 0; p0 < n; p0 += piece) {
+        const uint64_t cnt = std::min(piece, n - p0);
+        const uint8_t *b = (const uint8_t *)d_base + p0 * stride;
+        const Plan p = plan_strided(*D, C, (uint64_t)b, stride, len, cnt, kind, d_out_hdr != nullptr);
+        wc::LaunchArgs a{b,      stride, len,  nullptr,  nullptr, cnt,
+                         d_out ? d_out + p0 : nullptr,  d_bad,  kind, false,    p.full,  C.nt != 0,
+                         0,      d_out_hdr ? d_out_hdr + p0 : nullptr};
+        a.variant = C.variant;
+        rc = run(*D, C, a, p, (hipStream_t)stream);
+        if (rc)
+            return rc;
+    }
+    return WC_OK;
 }
 
 int batch_ragged(const void *d_base, const uint64_t *d_off, const uint16_t *d_len,
@@ -686,12 +697,19 @@ int batch_ragged(const void *d_base, const uint64_t *d_off, const uint16_t *d_le
     int rc = ensure_device(&D, &C);
     if (rc)
         return rc;
-    const Plan p = plan_ragged(*D, C, n, kind, false, d_out_hdr != nullptr);
-    wc::LaunchArgs a{d_base, 0,     0,    d_off, d_len, n,
-                     d_out,  d_bad, kind, true,  false, C.nt != 0, C.flat_tpw,
-                     d_out_hdr, C.diag_noload != 0};
-    a.variant = C.variant;
-    return run(*D, C, a, p, (hipStream_t)stream);
+    const uint64_t piece = C.split_pkts && n > C.split_pkts ? C.split_pkts : n;
+    for (uint64_t p0 = 0; p0 < n; p0 += piece) {
+        const uint64_t cnt = std::min(piece, n - p0);
+        const Plan p = plan_ragged(*D, C, cnt, kind, false, d_out_hdr != nullptr);
+        wc::LaunchArgs a{d_base, 0,     0,    d_off + p0, d_len + p0, cnt,
+                         d_out ? d_out + p0 : nullptr,  d_bad, kind, true,  false, C.nt != 0,
+                         C.flat_tpw, d_out_hdr ? d_out_hdr + p0 : nullptr, C.diag_noload != 0};
+        a.variant = C.variant;
+        rc = run(*D, C, a, p, (hipStream_t)stream);
+        if (rc)
+            return rc;
+    }
+    return WC_OK;
 }
 
 [[noreturn]] void die(const char *what, int rc)
