@@ -140,14 +140,14 @@ def main():
             lo = mhz[len(mhz) // 20] if mhz else float("nan")
             res[name].append(ms)
             clk[name].append(med)
-            print(f"round {r} {name:<10} {ms * 1e3:10.1f} us/call  {nbytes / ms / 1e9:7.1f} GB/s "
-                  f"= {nbytes / ms / 1e9 / 8000:.4f}  sclk median {med:6.0f} MHz (p5 {lo:6.0f})"
+            print(f"round {r} {name:<10} {ms * 1e3:10.1f} us/call  {nbytes / ms / 1e6:7.1f} GB/s "
+                  f"= {nbytes / ms / 1e6 / 8000:.4f}  sclk median {med:6.0f} MHz (p5 {lo:6.0f})"
                   f"  {iters} calls", flush=True)
     set_cap(None)
     print("== median over rounds")
     for name, (fn, nbytes, cap) in phases.items():
         ms = statistics.median(res[name])
-        print(f"{name:<10} {ms * 1e3:10.1f} us/call  {nbytes / ms / 1e9 / 8000:.4f} of 8 TB/s  "
+        print(f"{name:<10} {ms * 1e3:10.1f} us/call  {nbytes / ms / 1e6 / 8000:.4f} of 8 TB/s  "
               f"sclk {statistics.median(clk[name]):6.0f} MHz", flush=True)
     # parity of the last split round against the one-launch results: identical
     # bytes, identical checksums (a cheap self-check; the oracle checks live in

@@ -139,13 +139,13 @@ def main():
                     elif not torch.equal(ref[w], res):
                         print(f"!! {a} {w} {v!r}: results differ", flush=True)
                 print(f"  round {r} {a:<6} {w:>9} {v or 'default':<28} {ms * 1e3:10.1f} us "
-                      f"{w * L / ms / 1e9 / 8000 * 100:6.2f} %", flush=True)
+                      f"{w * L / ms / 1e6 / 8000 * 100:6.2f} %", flush=True)
     apply("")
     print("== median over rounds (frac of 8 TB/s)")
     for (a, w, v), ts in times.items():
         med = statistics.median(ts)
         print(f"{a:<6} {w:>9} {v or 'default':<28} {med * 1e3:10.1f} us  "
-              f"{w * L / med / 1e9:7.1f} GB/s  {w * L / med / 1e9 / 8000:.4f}", flush=True)
+              f"{w * L / med / 1e6:7.1f} GB/s  {w * L / med / 1e6 / 8000:.4f}", flush=True)
     for (a, w), (ptr, out) in bufs.items():
         if a != "torch":
             hip.hipFree(ctypes.c_void_p(ptr))
