@@ -501,6 +501,27 @@ def test_lean_phase_slots(gpu, monkeypatch, length, lean_phase):
         assert (plan["kernel"] == "lean") == want, (kind, plan)
 
 
+def test_split_bytes_strided(gpu, monkeypatch):
+    """WC_SPLIT_BYTES (the default splitter of strided batches, 3 GiB of
+    stride per launch) at small sizes: pieces of 64 KiB of stride."""
+    monkeypatch.setenv("WC_SPLIT_BYTES", str(1 << 16))
+    wc.reload_config()
+    try:
+        rng = np.random.default_rng(3)
+        n = 20000
+        for L, stride, at, kind in ((1472, 1472, 0, "ip"), (100, 2048, 14, "payload"),
+                                    (64, 64, 0, "ip"), (333, 333, 5, "payload")):
+            buf = rng.integers(0, 256, at + n * stride + 64, dtype=np.uint8)
+            got = host(wc.cksum_strided(dev_u8(buf, gpu), stride, L, n, kind=kind,
+                                        byte_offset=at))
+            want = c_oracle.cksum_strided(buf, stride, L, n, kind=0 if kind == "ip" else 1,
+                                          byte_offset=at)
+            np.testing.assert_array_equal(got, want, err_msg=f"{L} {stride} +{at} {kind}")
+    finally:
+        monkeypatch.delenv("WC_SPLIT_BYTES")
+        wc.reload_config()
+
+
 @pytest.mark.parametrize("piece", [1, 777, 4096])
 def test_split_launches(gpu, monkeypatch, piece):
     """WC_SPLIT_PKTS: a batch larger than the piece runs as back-to-back

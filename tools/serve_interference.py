@@ -29,6 +29,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import warpcore_amd as wc  # noqa: E402
+from warpcore_amd import _lib  # noqa: E402
 
 L = 1472
 
@@ -72,7 +73,7 @@ def main():
             if state == "none":
                 os.environ["WC_SERVE"] = "0"
                 wc.reload_config()
-                wc.gpu_fini()  # stops a running grid
+                _lib.load().wc_gpu_fini()  # stops a running grid
                 wc.gpu_init(0)
                 s0 = wc.server_stats()
                 assert (wc.cksum_host(pool, off, ln) == want).all()
@@ -107,18 +108,18 @@ def main():
                 s1 = wc.server_stats()
                 assert s1["fallbacks"] == s0["fallbacks"], (s0, s1)
             res[state].append(us)
-            print(f"round {r} {state:<5} C2 kernel {us:8.1f} us = {n * L / us / 1e6 / 8000:.4f}",
+            print(f"round {r} {state:<5} C2 kernel {us:8.1f} us = {n * L / us / 1e3 / 8000:.4f}",
                   flush=True)
     print("== median over rounds")
     base = statistics.median(res["none"])
     for state, v in res.items():
         m = statistics.median(v)
-        print(f"{state:<5} {m:8.1f} us  frac {n * L / m / 1e6 / 8000:.4f}  "
+        print(f"{state:<5} {m:8.1f} us  frac {n * L / m / 1e3 / 8000:.4f}  "
               f"({(m / base - 1) * 100:+.2f} % vs none)", flush=True)
     if calls:
         print(f"busy: {statistics.median(calls):.0f} server calls/s answered during C2", flush=True)
     wc.host_unregister(pool)
-    wc.gpu_fini()
+    _lib.load().wc_gpu_fini()
 
 
 if __name__ == "__main__":

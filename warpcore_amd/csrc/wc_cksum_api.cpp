@@ -163,7 +163,15 @@ struct Config {
     int flat_pk = 1;               // WC_FLAT_PK: flat kernel chunks per lane slot
     int gather = 1;                // WC_GATHER: seg kernel's gathered-stream path (0 off, 2 forced)
     int lean_max = 48;             // WC_LEAN_MAX: lean kernel for aligned packets up to this many chunks
-    uint64_t split_pkts = 0;       // WC_SPLIT_PKTS: batches above this many packets run as back-to-back launches of it
+    // Large batches as back-to-back launches (one launch of millions of
+    // one-shot workgroups lets the XCDs drift apart in the address space;
+    // DESIGN.md section 5.3): strided batches in pieces of WC_SPLIT_BYTES of
+    // stride (default 3 GiB: the 49-GB C5 window 0.907 -> 0.944 of peak,
+    // profiles/ab_r05_split.log), and, if set, any batch in pieces of
+    // WC_SPLIT_PKTS packets (ragged batches: off by default, C4 measured
+    // slower split).
+    uint64_t split_bytes = 3ull << 30; // WC_SPLIT_BYTES (0 = off)
+    uint64_t split_pkts = 0;           // WC_SPLIT_PKTS (0 = off; overrides WC_SPLIT_BYTES)
     int lean_phase = 1;            // WC_LEAN_PHASE: lean kernel for sparse packets at an even phase too
     int serve = 1;                 // WC_SERVE: resident server for small registered host batches
     int serve_waves = 64;          // WC_SERVE_WAVES: its waves (one 64-lane workgroup each)
@@ -265,6 +273,7 @@ void load_config_locked()
     c.flat_pk = env_int("WC_FLAT_PK", c.flat_pk);
     c.gather = env_int("WC_GATHER", c.gather);
     c.lean_max = env_int("WC_LEAN_MAX", c.lean_max);
+    c.split_bytes = env_u64("WC_SPLIT_BYTES", c.split_bytes);
     c.split_pkts = env_u64("WC_SPLIT_PKTS", c.split_pkts);
     c.lean_phase = env_int("WC_LEAN_PHASE", c.lean_phase);
     c.serve = env_int("WC_SERVE", c.serve);
@@ -664,9 +673,13 @@ int batch_strided(const void *d_base, uint64_t stride, uint16_t len, uint64_t n,
     int rc = ensure_device(&D, &C);
     if (rc)
         return rc;
-    // A batch larger than C.split_pkts runs as back-to-back launches of that
-    // many packets on the same stream (WC_SPLIT_PKTS; 0 = one launch).
-    const uint64_t piece = C.split_pkts && n > C.split_pkts && stride ? C.split_pkts : n;
+    // A batch larger than the piece runs as back-to-back launches of it on
+    // the same stream, each planned on its own (Config::split_bytes).
+    uint64_t piece = n;
+    if (C.split_pkts)
+        piece = std::min(n, C.split_pkts);
+    else if (C.split_bytes && stride)
+        piece = std::min(n, std::max<uint64_t>(1, C.split_bytes / stride));
     for (uint64_t p0 = 0; p0 < n; p0 += piece) {
         const uint64_t cnt = std::min(piece, n - p0);
         const uint8_t *b = (const uint8_t *)d_base + p0 * stride;
