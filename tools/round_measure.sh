@@ -27,6 +27,7 @@ for c in ${CFGS:-c2 c4 c4pl slotspl}; do
         zslotsf) a="--config zslots --fused" ;;
         rx) a="--config rx" ;;
         zrx) a="--config zrx" ;;
+        zrxa3) a="--config zrx --rx-arp 3" ;;
         c3pl_*) a="--config c3 --len ${c#c3pl_} --kind payload --headers" ;;
         s14_*) a="--config c3 --len ${c#s14_} --stride 2048 --offset 14" ;;
         s14pl_*) a="--config c3 --len ${c#s14pl_} --stride 2048 --offset 14 --kind payload --headers" ;;
