@@ -918,10 +918,10 @@ hipError_t rx_launch(Device &D, const Config &C, const void *base, const uint64_
     const int set = (int)(g % kRxSets);
     const uint64_t tiles = (n + 63) / 64;
     const uint32_t words = (uint32_t)std::min<uint64_t>((tiles + 63) / 64, wc::kRxTallyWords);
-    // words an earlier, larger launch left past this one's: cleared, so a
-    // 16-bit tag that comes round again never counts them
-    if (D.rx_words[set] > words)
-        memset(D.h_rx_tally[set] + words, 0, (D.rx_words[set] - words) * 4u);
+    // cleared first: a word older launches left there could carry this
+    // launch's 16-bit tag once the tags come round (a late store of launch
+    // g - 4 after the clear carries g - 4's tag and is not counted)
+    memset(D.h_rx_tally[set], 0, words * 4u);
     D.rx_words[set] = words;
     const int m = wc::kRxHdrT | (D.rx_early ? wc::kRxEarly : 0);
     return wc::launch_rx_verdict(base, offs, flens, n, verdict, drops, C.nt != 0, st, m,
