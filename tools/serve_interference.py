@@ -47,6 +47,7 @@ def main():
     buf = torch.empty(n * L + 64, dtype=torch.uint8, device=dev)
     wc.synth_fill(buf, 5, nbytes=n * L)
     out = torch.empty(n, dtype=torch.uint16, device=dev)
+    torch.cuda.synchronize()  # (before any server grid exists)
     pool = np.random.default_rng(3).integers(0, 256, 1 << 20, dtype=np.uint8)
     wc.host_register(pool)
     off = np.array([64], dtype=np.uint64)
@@ -55,9 +56,11 @@ def main():
     stream = torch.cuda.current_stream()
 
     def c2_us():
+        # stream synchronisation only: a device-wide one (torch.cuda.synchronize)
+        # waits for the resident server grid to be stopped
         for _ in range(20):
             wc.cksum_strided(buf, L, L, n, out=out)
-        torch.cuda.synchronize()
+        stream.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
         for _ in range(args.iters):

@@ -184,7 +184,8 @@ struct Config {
     int rx_early = 0;              // WC_RX_EARLY: RX verdict parses before streaming
     int rx_hdrt = 1;               // WC_RX_HDRT: RX verdict header chunks loaded transposed
     int rx_skip = 0;               // WC_RX_SKIP: frames the parse rules out leave the stream
-    int rx_adapt = 1;              // WC_RX_ADAPT: EARLY or HT per tile, by the ring's mix
+    int rx_adapt = 1;              // WC_RX_ADAPT: EARLY or HT per launch, by the ring's mix
+    int rx_trace = 0;              // WC_RX_TRACE: log each ADAPT decision to stderr (tools)
     int rx_mode() const
     {
         // The default: ADAPT (EARLY or the HT stream per tile, by the share
@@ -284,6 +285,7 @@ void load_config_locked()
     c.rx_hdrt = env_int("WC_RX_HDRT", c.rx_hdrt);
     c.rx_skip = env_int("WC_RX_SKIP", c.rx_skip);
     c.rx_adapt = env_int("WC_RX_ADAPT", c.rx_adapt);
+    c.rx_trace = env_int("WC_RX_TRACE", c.rx_trace);
     g_cfg = c;
     g_cfg_loaded = true;
 }
@@ -896,6 +898,8 @@ hipError_t rx_launch(Device &D, const Config &C, const void *base, const uint64_
     if (!(mode & wc::kRxAdapt) || !D.h_rx_tally[0])
         return wc::launch_rx_verdict(base, offs, flens, n, verdict, drops, C.nt != 0, st, mode);
     std::lock_guard<std::mutex> lk(g_rx_mu);
+    const auto t0 = std::chrono::steady_clock::now();
+    uint32_t from = 0, from_words = 0, from_seen = 0, from_out = 0;
     for (uint32_t back = 1; back < (uint32_t)kRxSets && back <= D.rx_gen; ++back) {
         const uint32_t g = D.rx_gen - back;
         const int set = (int)(g % kRxSets);
@@ -911,6 +915,10 @@ hipError_t rx_launch(Device &D, const Config &C, const void *base, const uint64_
         }
         if (words >= 8 || (words && words == D.rx_words[set])) {
             D.rx_early = out * 8u > seen;
+            from = g;
+            from_words = words;
+            from_seen = seen;
+            from_out = out;
             break;
         }
     }
@@ -924,6 +932,12 @@ hipError_t rx_launch(Device &D, const Config &C, const void *base, const uint64_
     memset(D.h_rx_tally[set], 0, words * 4u);
     D.rx_words[set] = words;
     const int m = wc::kRxHdrT | (D.rx_early ? wc::kRxEarly : 0);
+    if (C.rx_trace)
+        fprintf(stderr, "wccksum rx gen %u: %s (tally of gen %u: %u words, %u of %u frames ruled "
+                        "out; %.1f us on the host)\n",
+                g, D.rx_early ? "EARLY" : "HT", from, from_words, from_out, from_seen,
+                std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0)
+                    .count());
     return wc::launch_rx_verdict(base, offs, flens, n, verdict, drops, C.nt != 0, st, m,
                                  D.d_rx_tally[set], g & 0xFFFFu);
 }
