@@ -19,7 +19,7 @@ KEYS = {"c2": "c2:1472", "c2pl": "c2:1472:payload:headers", "c4": "c4:zipf",
         "zslotspl": "zslots:zipf:payload:headers",
         "c2f": "c2:1472:payload:headers:fused", "c4f": "c4:zipf:payload:headers:fused",
         "slotsf": "slots:1500:payload:headers:fused",
-        "zslotsf": "zslots:zipf:payload:headers:fused", "rx": "rx:1514", "zrx": "zrx:zipf"}
+        "zslotsf": "zslots:zipf:payload:headers:fused", "rx": "rx:1514", "zrx": "zrx:zipf", "c5": "c5:1472", "zrxa3": "zrx:zipf:arp3"}
 
 
 def main():
