@@ -85,7 +85,8 @@ def parse(argv=None):
                     help="skip the C5 strong-scaling leg every line carries by default")
     ap.add_argument("--no-extra", action="store_true",
                     help="skip the c3 / c4 objects and C2's frac_rotating")
-    ap.add_argument("--c5-steps", type=int, default=3, help="timed steps of the C5 leg")
+    ap.add_argument("--c5-steps", type=int, default=3,
+                    help="at least this many timed steps of the C5 leg (and >= 0.5 s)")
     ap.add_argument("--headers", action="store_true",
                     help="stamp well-formed IPv4 / IPv6 UDP headers on every packet "
                          "(synth.stamp_udp_headers) instead of random header bytes")
@@ -648,21 +649,30 @@ def c5_leg(args, dev, rank, world, coll_dev):
         for c in counts:
             wc.cksum_strided(buf, L, L, c, out=out, kind="ip")
 
-    step()
-    torch.cuda.synchronize(dev)
+    # Warm up for >= 0.3 s (the clock ramps; a fresh 49-GB window's first
+    # pass), then time at least --c5-steps steps and >= 0.5 s of them (one
+    # step is 55 ms at N = 1 but 7 ms at N = 8).
+    t_w = time.perf_counter()
+    warm = 0
+    while warm < 1 or time.perf_counter() - t_w < 0.3:
+        step()
+        torch.cuda.synchronize(dev)
+        warm += 1
+    step_s = (time.perf_counter() - t_w) / warm
+    steps = int(wdist.max_over_ranks(float(max(args.c5_steps, -(-0.5 // step_s))), coll_dev))
     wdist.barrier(dev)
     stream = torch.cuda.current_stream(dev)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)
-    for _ in range(args.c5_steps):
+    for _ in range(steps):
         step()
     ev1.record(stream)
     wdist.barrier(dev)
     elapsed = wdist.max_over_ranks(time.perf_counter() - t0, coll_dev)
-    kernel_ms = wdist.max_over_ranks(ev0.elapsed_time(ev1) / args.c5_steps / launches, coll_dev)
-    total_bytes = float(args.total_packets) * L * args.c5_steps
+    kernel_ms = wdist.max_over_ranks(ev0.elapsed_time(ev1) / steps / launches, coll_dev)
+    total_bytes = float(args.total_packets) * L * steps
     gbps = total_bytes / elapsed / 1e9
     # sampled parity: every launch rewrote out[:count] from the same window
     m = min(1 << 16, counts[-1])
@@ -680,8 +690,8 @@ def c5_leg(args, dev, rank, world, coll_dev):
                      f"{args.total_packets * L / 1e9:.1f} GB in total, split evenly over "
                      f"{world} rank(s): {share} packets per rank as {launches} launch(es) over "
                      f"a resident {win}-packet window"),
-        "scaling": "strong", "n_gpus": world, "steps": args.c5_steps,
-        "ms_per_step": round(elapsed / args.c5_steps * 1e3, 3),
+        "scaling": "strong", "n_gpus": world, "steps": steps, "warmup_steps": warm,
+        "ms_per_step": round(elapsed / steps * 1e3, 3),
         "value": round(total_bytes / elapsed / GIB, 2), "unit": "GiB/s",
         "GBps": round(gbps, 1),
         "frac_job": round(gbps / (world * HBM_PEAK_GBPS), 4),
