@@ -103,3 +103,35 @@ def test_argument_errors_need_no_gpu():
     assert lib.wc_cksum_strided(p, 2048, 64, 8, p, 7, None) == einval
     assert lib.wc_cksum_ragged(p, p, p, 8, p, -1, None) == einval
     assert lib.wc_strerror(einval).decode() == "invalid argument"
+
+
+def test_host_call_argument_errors_need_no_gpu():
+    """The host-memory calls check their batch against the region before
+    touching a device: NULL result arrays, packets past the region -- for the
+    fused pair also an IPv4 header (hl bytes, options included) that runs past
+    it even where len is shorter -- are WC_EINVAL; an empty batch is WC_OK;
+    wc_server_stats needs no device either."""
+    import ctypes
+
+    import numpy as np
+    lib = _lib.load()
+    ok, einval = 0, -10001
+    buf = np.zeros(100, dtype=np.uint8)
+    off = np.array([50], dtype=np.uint64)
+    ln = np.array([20], dtype=np.uint16)
+    out = np.zeros(1, dtype=np.uint16)
+    hdr = np.zeros(1, dtype=np.uint16)
+    b, o, n_, r, h = (a.ctypes.data for a in (buf, off, ln, out, hdr))
+    assert lib.wc_cksum_ip_udp_host(b, 100, o, n_, 0, None, None) == ok
+    assert lib.wc_cksum_ip_udp_host(b, 100, o, n_, 1, None, r) == einval
+    assert lib.wc_cksum_ip_udp_host(b, 100, o, n_, 1, h, None) == einval
+    assert lib.wc_cksum_host(b, 100, o, n_, 1, None, 0) == einval
+    off[0] = 90  # 20 bytes from 90: past the 100-byte region
+    assert lib.wc_cksum_host(b, 100, o, n_, 1, r, 0) == einval
+    assert lib.wc_cksum_ip_udp_host(b, 100, o, n_, 1, h, r) == einval
+    off[0] = 50
+    buf[50] = 0x4F  # IPv4, IHL 15: ip_cksum reads 60 bytes, 50 are left
+    assert lib.wc_cksum_ip_udp_host(b, 100, o, n_, 1, h, r) == einval
+    vals = [ctypes.c_uint64(7) for _ in range(3)]
+    assert lib.wc_server_stats(*[ctypes.byref(v) for v in vals]) == ok
+    assert lib.wc_server_stats(None, None, None) == ok
