@@ -91,6 +91,9 @@ def main():
                          "(HBM, not the 256 MiB Infinity Cache)")
     ap.add_argument("--rx-arp", type=int, default=0,
                     help="rx / zrx: every K-th frame an ARP frame (no UDP check)")
+    ap.add_argument("--rx-packed", action="store_true",
+                    help="rx / zrx: the frames back to back (C4's layout) instead of one per "
+                         "2048-B slot")
     ap.add_argument("--ragged", action="store_true",
                     help="c2/c3 through the ragged entry point (offset/length arrays)")
     args = ap.parse_args()
@@ -106,7 +109,7 @@ def main():
                    else synth.zipf_lengths(n))
         buf = torch.empty(n * 2048 + 64, dtype=torch.uint8, device=dev)
         wc.synth_fill(buf, 1, nbytes=n * 2048)
-        f_off, f_len = synth.make_rx_ring(buf, n, ip_lens)
+        f_off, f_len = synth.make_rx_ring(buf, n, ip_lens, packed=args.rx_packed)
         if args.rx_arp:
             sel = torch.from_numpy(f_off[::args.rx_arp].astype(np.int64)).to(dev)
             buf[sel + 12] = 0x08

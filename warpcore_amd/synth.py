@@ -34,7 +34,7 @@ def packed_offsets(lengths: np.ndarray, lead: int = 0) -> np.ndarray:
     return off
 
 
-def make_rx_ring(buf, n: int, ip_lens, slot: int = 2048, v6_every: int = 3):
+def make_rx_ring(buf, n: int, ip_lens, slot: int = 2048, v6_every: int = 3, packed: bool = False):
     """A netmap RX ring of well-formed UDP frames in `buf` (uint8 device
     tensor of >= n * slot bytes, already filled with synthetic bytes): frame i
     in slot i, an Ethernet header (random MACs, EtherType per version,
@@ -42,6 +42,8 @@ def make_rx_ring(buf, n: int, ip_lens, slot: int = 2048, v6_every: int = 3):
     datagram of ip_lens[i] bytes at +14 (stamp_udp_headers), its IPv4 header
     checksum and UDP checksum computed on the device (wc_cksum_ip_udp_ragged)
     and stored raw, as mk_ip4_hdr / udp_tx do (ip4.c:184-186, udp.c:209-213).
+    `packed`: frames back to back instead (frame i right after frame i - 1,
+    any alignment; `buf` needs >= sum of the frame lengths).
     Returns (frame offsets uint64, frame lengths uint16) as numpy arrays."""
     import torch
 
@@ -49,8 +51,9 @@ def make_rx_ring(buf, n: int, ip_lens, slot: int = 2048, v6_every: int = 3):
 
     dev = buf.device
     ip_lens = np.asarray(ip_lens, dtype=np.uint16)
-    f_off = (np.arange(n, dtype=np.uint64) * slot).astype(np.uint64)
     f_len = (ip_lens.astype(np.int64) + 14).astype(np.uint16)
+    f_off = (packed_offsets(f_len) if packed
+             else (np.arange(n, dtype=np.uint64) * slot).astype(np.uint64))
     d_foff = torch.from_numpy(f_off.astype(np.int64)).to(dev)
     d_ipoff = d_foff + 14
     d_iplen = torch.from_numpy(ip_lens.astype(np.int64)).to(dev)
