@@ -140,9 +140,9 @@ PLANNED = [
     (0, 256, 256, "ip", (8, 2, 2)),           # lean kernel, the pass filled exactly
     (0, 576, 576, "ip", (16, 3, 1)),
     (0, 9000, 9000, "ip", (32, 18, 1)),
-    (14, 2048, 64, "ip", (8, 1, 4)),          # small packets in netmap slots (lean, PH)
-    (14, 2048, 64, "payload", (8, 1, 4)),
-    (14, 2048, 128, "ip", (8, 2, 4)),
+    (14, 2048, 64, "ip", (8, 1, 4)),          # small packets in netmap slots: group kernel
+    (14, 2048, 128, "ip", (8, 3, 2)),         # (ip_cksum gains nothing on the PH path)
+    (14, 2048, 64, "payload", (8, 1, 4)),     # payload_cksum: lean kernel, PH path
     (14, 2048, 128, "payload", (8, 2, 4)),
     (14, 2048, 240, "payload", (8, 2, 4)),
 ]
