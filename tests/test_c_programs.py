@@ -9,7 +9,8 @@ from cprog import build
 
 
 @pytest.mark.parametrize("name", ["rx_ring_loop", "host_latency", "dropin_test",
-                                  "multi_test", "sock_verify", "tx_queue_loop"])
+                                  "multi_test", "sock_verify", "tx_queue_loop",
+                                  "thread_engines"])
 def test_c_program_builds(name, tmp_path):
     assert build(name, tmp_path).exists()
 

@@ -205,3 +205,20 @@ def test_c_tx_queue_loop(gpu, tmp_path):
     r = subprocess.run([str(exe), "2"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "tx_queue_loop: ok" in r.stdout
+
+
+def test_c_thread_engines(gpu, tmp_path):
+    """Several engines on their own threads call the library at once
+    (tests/c/thread_engines.c): host engines over registered and pageable
+    buffer regions (server, zero-copy, pipeline; ip / payload / fused / RX
+    verdicts), device engines on their own streams (strided / ragged / fused /
+    RX), the scalar drop-in, and a thread that keeps registering and
+    unregistering a region (each stops the server grid).  Every result equals
+    the oracle's, and the server answered with no fallback."""
+    import subprocess
+
+    from cprog import build
+    exe = build("thread_engines", tmp_path)
+    r = subprocess.run([str(exe), "4", "4", "2"], capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "thread_engines: ok" in r.stdout
