@@ -23,12 +23,15 @@
  *
  *   thread_engines [seconds] [host_engines] [device_engines]
  */
+#include <execinfo.h>
 #include <pthread.h>
+#include <signal.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <unistd.h>
 
 #include <hip/hip_runtime_api.h>
 
@@ -82,6 +85,15 @@ static void frame_hdr(uint8_t *f, uint64_t r)
     }
 }
 
+/* payload_cksum is defined for len >= the header length only (the reference
+ * converts len - hl to uint32: a shorter len reads ~4 GiB past the packet,
+ * in_cksum.c:160-165), so payload lengths are raised to it. */
+static uint16_t payload_len(const uint8_t *pk, uint16_t len)
+{
+    const uint16_t hl = (pk[0] >> 4) == 4 ? (uint16_t)((pk[0] & 15u) * 4u) : 40u;
+    return len < hl ? hl : len;
+}
+
 struct result {
     uint64_t calls, packets, bad;
 };
@@ -127,6 +139,8 @@ static void *host_engine(void *p)
             const uint64_t b = xs(&s) % NBUF;
             off[i] = b * BUF;
             len[i] = (uint16_t)(xs(&s) % 1515);
+            if (op == 1 || op == 2)
+                len[i] = payload_len(mem + off[i], len[i]);
             if (op == 3) /* a fresh frame header for this buffer */
                 frame_hdr(mem + off[i], xs(&s));
         }
@@ -238,7 +252,9 @@ static void *device_engine(void *p)
         const int op = (int)(it % 4);
         uint64_t n;
         uint16_t L = (uint16_t)(1 + xs(&s) % 1500);
-        uint64_t stride = L + xs(&s) % 64;
+        if (op == 0 && (it / 4) % 2 && L < 60) /* payload: L >= any header length */
+            L = 60;
+        const uint64_t stride = L + xs(&s) % 64;
         int rc;
         if (op == 0) { /* strided, packed or sparse */
             n = 1 + xs(&s) % (DBYTES / stride - 1);
@@ -251,6 +267,8 @@ static void *device_engine(void *p)
             for (uint64_t i = 0; i < n; ++i) {
                 h_off[i] = (xs(&s) % (DBYTES / BUF)) * BUF + (op == 3 ? 0 : xs(&s) % 64);
                 h_len[i] = (uint16_t)(xs(&s) % 1515);
+                if (op == 2 || (op == 1 && (it / 4) % 2))
+                    h_len[i] = payload_len(h_buf + h_off[i], h_len[i]);
             }
             ok = hip_ok(hipMemcpyAsync(d_off, h_off, n * 8, hipMemcpyHostToDevice, st), a->id,
                         "H2D") &&
@@ -331,9 +349,11 @@ static void *scalar_caller(void *p)
     uint8_t buf[2048];
     const double t_end = now_s() + g_seconds;
     while (!g_stop && now_s() < t_end) {
-        const uint16_t l = (uint16_t)(xs(&s) % 1515);
+        uint16_t l = (uint16_t)(xs(&s) % 1515);
         fill(buf, sizeof buf, &s);
         const int pay = (int)(r->calls & 1);
+        if (pay)
+            l = payload_len(buf, l);
         const uint16_t got = pay ? payload_cksum(buf, l) : ip_cksum(buf, l);
         const uint16_t w = pay ? oracle_payload_cksum(buf, l) : oracle_ip_cksum(buf, l);
         if (got != w && r->bad++ < 5)
@@ -367,8 +387,24 @@ static void *churn(void *p)
     return NULL;
 }
 
+/* A crash names its place: the backtrace (library frames as lib(+offset)
+ * for addr2line) on stderr, then the signal's exit status. */
+static void on_fault(int sig)
+{
+    void *bt[64];
+    const int n = backtrace(bt, 64);
+    static const char msg[] = "thread_engines: fatal signal, backtrace:\n";
+    (void)!write(2, msg, sizeof msg - 1);
+    backtrace_symbols_fd(bt, n, 2);
+    _exit(128 + sig);
+}
+
 int main(int argc, char **argv)
 {
+    setvbuf(stdout, NULL, _IOLBF, 0);
+    signal(SIGSEGV, on_fault);
+    signal(SIGBUS, on_fault);
+    signal(SIGABRT, on_fault);
     if (argc > 1)
         g_seconds = atof(argv[1]);
     const int nh = argc > 2 ? atoi(argv[2]) : 4, nd = argc > 3 ? atoi(argv[3]) : 2;
