@@ -387,6 +387,17 @@ static void *churn(void *p)
     return NULL;
 }
 
+/* Every engine must have been served in turn: the library's lock is first
+ * come, first served, and device-resident calls do not wait for it. */
+static int starved(const char *who, int id, uint64_t calls, uint64_t min_calls)
+{
+    if (calls >= min_calls)
+        return 0;
+    fprintf(stderr, "%s %d: only %llu calls in %.1f s (starved)\n", who, id,
+            (unsigned long long)calls, g_seconds);
+    return 1;
+}
+
 /* A crash names its place: the backtrace (library frames as lib(+offset)
  * for addr2line) on stderr, then the signal's exit status. */
 static void on_fault(int sig)
@@ -442,17 +453,18 @@ int main(int argc, char **argv)
         printf("  host %d (%s): %llu calls, %llu packets, %llu mismatches\n", i,
                ha[i].registered ? "registered" : "pageable", (unsigned long long)ha[i].r.calls,
                (unsigned long long)ha[i].r.packets, (unsigned long long)ha[i].r.bad);
-        bad += ha[i].r.bad + (ha[i].r.calls == 0);
+        bad += ha[i].r.bad + starved("host", i, ha[i].r.calls, 20);
     }
     for (int i = 0; i < nd; ++i) {
         printf("  device %d: %llu calls, %llu packets, %llu mismatches\n", i,
                (unsigned long long)da[i].r.calls, (unsigned long long)da[i].r.packets,
                (unsigned long long)da[i].r.bad);
-        bad += da[i].r.bad + (da[i].r.calls == 0);
+        bad += da[i].r.bad + starved("device", i, da[i].r.calls, 20);
     }
     printf("  scalar: %llu calls, %llu mismatches; churn: %llu register cycles\n",
            (unsigned long long)sc.calls, (unsigned long long)sc.bad,
            (unsigned long long)ch.calls);
+    bad += starved("scalar", 0, sc.calls, 20) + starved("churn", 0, ch.calls, 5);
     uint64_t served = 0, fb = 0, l = 0;
     wc_server_stats(&served, &fb, &l);
     printf("  server: %llu batches served, %llu fallbacks, %llu grid launches\n",

@@ -136,7 +136,8 @@ struct Registration {
 // Tuning knobs (the WC_* environment), read once when the library first
 // initialises and again only on wc_config_reload(); the defaults are the
 // values tuned on MI355X (DESIGN.md sections 4-5).  Batch calls take a copy
-// under g_mu, so a reload never races a launch.
+// under g_cfg_mu (written with g_mu and g_cfg_mu held), so a reload never
+// races a launch.
 struct Config {
     int blocks_per_cu = 0;         // WC_BLOCKS_PER_CU: cap the one-shot grid
     int grid = 0;                  // WC_GRID: fixed grid (grid-stride)
@@ -201,8 +202,49 @@ struct Config {
     }
 };
 
-std::mutex g_mu;
+// The library lock: first come, first served.  Host-memory batch calls hold
+// it for a whole call (the server, zero-copy and pipeline resources are the
+// device's), and several engine threads may call back to back; a plain
+// std::mutex let the thread that had just released it take it again, and one
+// engine starved the others for seconds (tests/c/thread_engines.c: 123,710
+// calls on one thread, 2-4 on each of seven others).  A ticket order, with a
+// short spin before sleeping (the server answers in ~5 us).
+class FairMutex {
+public:
+    void lock()
+    {
+        const uint64_t t = next_.fetch_add(1, std::memory_order_relaxed);
+        for (int spin = 0; spin < 4096; ++spin) {
+            if (serving_.load(std::memory_order_acquire) == t)
+                return;
+            __builtin_ia32_pause();
+        }
+        std::unique_lock<std::mutex> l(m_);
+        cv_.wait(l, [&] { return serving_.load(std::memory_order_acquire) == t; });
+    }
+    void unlock()
+    {
+        {
+            std::lock_guard<std::mutex> l(m_); // (no lost wake-up between test and wait)
+            serving_.fetch_add(1, std::memory_order_release);
+        }
+        cv_.notify_all();
+    }
+
+private:
+    std::atomic<uint64_t> next_{0}, serving_{0};
+    std::mutex m_;
+    std::condition_variable cv_;
+};
+
+FairMutex g_mu;
 Device g_dev[kMaxDevices];
+// Device d's state is built (set under g_mu once init_locked has finished it,
+// cleared by wc_gpu_fini): device-resident batch calls then only copy the
+// configuration (g_cfg_mu) and enqueue on the caller's stream, without
+// queueing behind a host-memory call that holds g_mu.
+std::atomic<bool> g_dev_ready[kMaxDevices];
+std::mutex g_cfg_mu; // g_cfg is written with g_mu AND g_cfg_mu held
 std::map<uintptr_t, Registration> g_registered; // host base -> region
 Config g_cfg;
 bool g_cfg_loaded = false;
@@ -286,7 +328,10 @@ void load_config_locked()
     c.rx_skip = env_int("WC_RX_SKIP", c.rx_skip);
     c.rx_adapt = env_int("WC_RX_ADAPT", c.rx_adapt);
     c.rx_trace = env_int("WC_RX_TRACE", c.rx_trace);
-    g_cfg = c;
+    {
+        std::lock_guard<std::mutex> lk(g_cfg_mu);
+        g_cfg = c;
+    }
     g_cfg_loaded = true;
 }
 
@@ -360,17 +405,30 @@ int init_locked(int device, Device **out)
             memset(D.h_rx_tally[k], 0, wc::kRxTallyWords * 4);
         }
         D.ok = true;
+        g_dev_ready[device].store(true, std::memory_order_release);
     }
     *out = &D;
     return WC_OK;
 }
 
+// The device-resident batch calls' entry: the current device's state and a
+// copy of the configuration.  Once the device is set up this takes only the
+// configuration lock (held for the copy), never g_mu.
 int ensure_device(Device **out, Config *cfg)
 {
-    std::lock_guard<std::mutex> lk(g_mu);
-    const int rc = init_locked(-1, out);
-    if (rc == WC_OK)
+    int dev = 0;
+    if (current_device(&dev) == WC_OK && g_dev_ready[dev].load(std::memory_order_acquire)) {
+        *out = &g_dev[dev];
+        std::lock_guard<std::mutex> lk(g_cfg_mu);
         *cfg = g_cfg;
+        return WC_OK;
+    }
+    std::lock_guard<FairMutex> lk(g_mu);
+    const int rc = init_locked(-1, out);
+    if (rc == WC_OK) {
+        std::lock_guard<std::mutex> lc(g_cfg_mu);
+        *cfg = g_cfg;
+    }
     return rc;
 }
 
@@ -735,7 +793,7 @@ int batch_ragged(const void *d_base, const uint64_t *d_off, const uint16_t *d_le
 
 uint16_t scalar_cksum(const void *buf, uint16_t len, int kind, const char *who)
 {
-    std::lock_guard<std::mutex> lk(g_mu);
+    std::lock_guard<FairMutex> lk(g_mu);
     Device *D = nullptr;
     int rc = init_locked(-1, &D);
     if (rc)
@@ -1048,7 +1106,7 @@ void server_watch()
 {
     while (!g_srv_quit.load()) {
         std::this_thread::sleep_for(std::chrono::milliseconds(2));
-        std::lock_guard<std::mutex> lk(g_mu);
+        std::lock_guard<FairMutex> lk(g_mu);
         const auto now = std::chrono::steady_clock::now();
         for (int d = 0; d < kMaxDevices; ++d) {
             Device &D = g_dev[d];
@@ -1064,7 +1122,7 @@ void server_atexit()
     g_srv_quit.store(true);
     if (g_srv_watcher.joinable())
         g_srv_watcher.join();
-    std::lock_guard<std::mutex> lk(g_mu);
+    std::lock_guard<FairMutex> lk(g_mu);
     server_stop_all_locked();
 }
 
@@ -1550,7 +1608,7 @@ int for_each_shard(F &&fn)
     int devs[kMaxDevices];
     int G = 0;
     {
-        std::lock_guard<std::mutex> lk(g_mu);
+        std::lock_guard<FairMutex> lk(g_mu);
         G = g_multi_n;
         for (int g = 0; g < G; ++g)
             devs[g] = g_shard[g].dev;
@@ -1588,7 +1646,7 @@ int host_batch(const void *h_base, uint64_t h_bytes, const uint64_t *h_off,
                        &total))
         return WC_EINVAL;
 
-    std::lock_guard<std::mutex> lk(g_mu);
+    std::lock_guard<FairMutex> lk(g_mu);
     Device *D = nullptr;
     int rc = init_locked(-1, &D);
     if (rc)
@@ -1690,7 +1748,7 @@ int wc_host_register(void *h_ptr, uint64_t bytes)
 {
     if (!h_ptr || !bytes)
         return WC_EINVAL;
-    std::lock_guard<std::mutex> lk(g_mu);
+    std::lock_guard<FairMutex> lk(g_mu);
     Device *D = nullptr;
     int rc = init_locked(-1, &D);
     if (rc)
@@ -1744,7 +1802,7 @@ int wc_host_unregister(void *h_ptr)
 {
     if (!h_ptr)
         return WC_EINVAL;
-    std::lock_guard<std::mutex> lk(g_mu);
+    std::lock_guard<FairMutex> lk(g_mu);
     auto it = g_registered.find((uintptr_t)h_ptr);
     if (it == g_registered.end())
         return WC_EINVAL;
@@ -1773,7 +1831,7 @@ int wc_cksum_ip_udp_host(const void *h_base, uint64_t h_bytes, const uint64_t *h
 
 int wc_server_stats(uint64_t *served, uint64_t *fallbacks, uint64_t *launches)
 {
-    std::lock_guard<std::mutex> lk(g_mu);
+    std::lock_guard<FairMutex> lk(g_mu);
     if (served)
         *served = g_srv_stats.served;
     if (fallbacks)
@@ -1830,7 +1888,7 @@ int wc_shard_range(uint64_t n, int g, int ngpus, uint64_t *lo, uint64_t *hi)
 
 int wc_gpu_init_multi(int ngpus, const int *devices)
 {
-    std::lock_guard<std::mutex> lk(g_mu);
+    std::lock_guard<FairMutex> lk(g_mu);
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
         return WC_ENODEV;
@@ -1887,7 +1945,7 @@ int wc_gpu_init_multi(int ngpus, const int *devices)
 
 int wc_gpu_multi_count(void)
 {
-    std::lock_guard<std::mutex> lk(g_mu);
+    std::lock_guard<FairMutex> lk(g_mu);
     return g_multi_n;
 }
 
@@ -1902,7 +1960,7 @@ int wc_cksum_host_multi(const void *h_base, uint64_t h_bytes, const uint64_t *h_
         return WC_EINVAL;
     int G = 0;
     {
-        std::lock_guard<std::mutex> lk(g_mu);
+        std::lock_guard<FairMutex> lk(g_mu);
         G = g_multi_n;
     }
     if (G == 0)
@@ -1913,7 +1971,7 @@ int wc_cksum_host_multi(const void *h_base, uint64_t h_bytes, const uint64_t *h_
                        &total))
         return WC_EINVAL;
     {
-        std::lock_guard<std::mutex> lk(g_mu);
+        std::lock_guard<FairMutex> lk(g_mu);
         G = g_multi_n;
         int cur = 0;
         if (hipGetDevice(&cur) != hipSuccess)
@@ -2006,7 +2064,7 @@ int wc_gather_results_multi(uint16_t *const *d_shard_out, const uint64_t *n,
 {
     if (!d_shard_out || !n || !d_all)
         return WC_EINVAL;
-    std::lock_guard<std::mutex> lk(g_mu);
+    std::lock_guard<FairMutex> lk(g_mu);
     if (g_multi_n == 0)
         return WC_EINVAL;
     int devs[kMaxDevices];
@@ -2022,16 +2080,18 @@ int wc_gather_results_multi(uint16_t *const *d_shard_out, const uint64_t *n,
 
 int wc_gpu_init(int device)
 {
-    std::lock_guard<std::mutex> lk(g_mu);
+    std::lock_guard<FairMutex> lk(g_mu);
     Device *D = nullptr;
     return init_locked(device, &D);
 }
 
 int wc_gpu_fini(void)
 {
-    std::lock_guard<std::mutex> lk(g_mu);
+    std::lock_guard<FairMutex> lk(g_mu);
     int cur = 0;
     const bool have_cur = hipGetDevice(&cur) == hipSuccess;
+    for (int d = 0; d < kMaxDevices; ++d) // (device calls take the locked path again)
+        g_dev_ready[d].store(false, std::memory_order_release);
     server_stop_all_locked();
     wc::rccl_fini();
     for (int g = 0; g < g_multi_n; ++g) {
@@ -2081,7 +2141,7 @@ int wc_gpu_fini(void)
 
 int wc_config_reload(void)
 {
-    std::lock_guard<std::mutex> lk(g_mu);
+    std::lock_guard<FairMutex> lk(g_mu);
     load_config_locked();
     return WC_OK;
 }
