@@ -1027,6 +1027,64 @@ def test_host_resident_server(gpu, monkeypatch, waves):
         wc.reload_config()
 
 
+def test_host_server_grid_holds_up_no_other_stream(gpu, monkeypatch):
+    """While the resident grid runs, work on other streams is not queued
+    behind it: HIP shares a few hardware queues among a process's streams,
+    and a command behind the never-ending grid on the same queue would wait
+    for it to leave (up to its 4-s drain, the idle watcher being held off
+    here).  With the grid up: a device batch on each of 12 new streams, each
+    synchronised on its stream alone, the zero-copy launch path (a batch past
+    the server's size) and the scalar drop-in all finish at once, and the grid
+    is still the same one afterwards (no relaunch)."""
+    import time
+    monkeypatch.setenv("WC_SERVE_IDLE_US", "30000000")  # the watcher stays out of it
+    wc.reload_config()
+    rng = np.random.default_rng(78)
+    slot = 2048
+    pool = rng.integers(0, 256, 2048 * slot, dtype=np.uint8)
+    wc.host_register(pool)
+    try:
+        one_off = np.array([5], dtype=np.uint64)
+        one_len = np.array([700], dtype=np.uint16)
+        want1 = c_oracle.cksum_ragged(pool, one_off, one_len)
+        np.testing.assert_array_equal(wc.cksum_host(pool, one_off, one_len), want1)  # grid up
+        s0 = wc.server_stats()
+        n, L = 4096, 1472
+        buf = torch.empty(n * L + 64, dtype=torch.uint8, device=gpu)
+        wc.synth_fill(buf, 9, nbytes=n * L)
+        streams = [torch.cuda.Stream(device=gpu) for _ in range(12)]
+        outs = [torch.empty(n, dtype=torch.uint16, device=gpu) for _ in streams]
+        torch.cuda.current_stream(gpu).synchronize()  # (the fill; a stream sync)
+        t0 = time.monotonic()
+        for st, o in zip(streams, outs):
+            wc.cksum_strided(buf, L, L, n, out=o, stream=st)
+        for st in streams:
+            st.synchronize()
+        dt_dev = time.monotonic() - t0
+        want = c_oracle.cksum_strided(buf[: n * L].cpu().numpy(), L, L, n)
+        for o in outs:
+            np.testing.assert_array_equal(o.cpu().numpy(), want)
+        offs = (np.arange(1500, dtype=np.uint64) * slot + 3).astype(np.uint64)
+        lens = rng.integers(0, 1500, 1500).astype(np.uint16)
+        t1 = time.monotonic()
+        got = wc.cksum_host(pool, offs, lens)  # > WC_SERVE_MAX: the zero-copy launch
+        dt_zc = time.monotonic() - t1
+        np.testing.assert_array_equal(got, c_oracle.cksum_ragged(pool, offs, lens))
+        pkt = pool[:1200].copy()
+        t2 = time.monotonic()
+        assert wc.ip_cksum(pkt) == c_oracle.ip_cksum(pkt)
+        dt_sc = time.monotonic() - t2
+        np.testing.assert_array_equal(wc.cksum_host(pool, one_off, one_len), want1)
+        s1 = wc.server_stats()
+        assert dt_dev < 0.5 and dt_zc < 0.5 and dt_sc < 0.5, (dt_dev, dt_zc, dt_sc)
+        assert s1["served"] - s0["served"] == 1, (s0, s1)
+        assert (s1["fallbacks"], s1["launches"]) == (s0["fallbacks"], s0["launches"]), (s0, s1)
+    finally:
+        wc.host_unregister(pool)
+        monkeypatch.delenv("WC_SERVE_IDLE_US")
+        wc.reload_config()
+
+
 def test_host_server_light_traffic_then_full_batch(gpu, monkeypatch):
     """under steady light traffic (1-packet calls, every
     other wave never sees a request) past the grid's own 4-s drain time, a

@@ -178,6 +178,8 @@ struct Config {
     int serve_waves = 64;          // WC_SERVE_WAVES: its waves (one 64-lane workgroup each)
     int serve_max = 256;           // WC_SERVE_MAX: largest batch (packets) it takes
     int serve_idle_us = 20000;     // WC_SERVE_IDLE_US: stopped after this long without a call
+    int serve_prio = 1;            // WC_SERVE_PRIO=0: its stream at normal priority (the A/B of
+                                   // server_stream_create; other streams then queue behind it)
     // RX verdict kernel modes (profiles/ab_r04_rx_*.log): transposed header
     // loads win everywhere (mixed ring 127.5 -> 111.4 us); parsing first
     // (EARLY) wins when many frames need no UDP check (a third ARP: 111.8 ->
@@ -323,6 +325,7 @@ void load_config_locked()
     c.serve_waves = std::max(1, std::min(env_int("WC_SERVE_WAVES", c.serve_waves), 1024));
     c.serve_max = std::max(0, std::min(env_int("WC_SERVE_MAX", c.serve_max), (int)wc::kSrvMaxPkts));
     c.serve_idle_us = std::max(100, env_int("WC_SERVE_IDLE_US", c.serve_idle_us));
+    c.serve_prio = env_int("WC_SERVE_PRIO", c.serve_prio) != 0;
     c.rx_early = env_int("WC_RX_EARLY", c.rx_early);
     c.rx_hdrt = env_int("WC_RX_HDRT", c.rx_hdrt);
     c.rx_skip = env_int("WC_RX_SKIP", c.rx_skip);
@@ -1036,12 +1039,35 @@ std::atomic<bool> g_srv_quit{false};
 std::thread g_srv_watcher;
 bool g_srv_hooks = false; // watcher started, atexit registered
 
-int server_init_locked(Server &S)
+// The grid's stream must not share a hardware queue with other work.  HIP
+// maps a process's streams onto a few shared hardware queues per priority
+// level (GPU_MAX_HW_QUEUES, 4 here), and a queue runs its commands in order:
+// every kernel or copy of another stream that lands on the grid's queue waits
+// until the grid leaves -- and the idle watcher that stops it needs g_mu,
+// which a host call waiting for such a kernel holds, so the wait lasted until
+// the grid's own 4-s drain (tests/c/thread_engines.c: 2-3 host calls per
+// engine in 8 s).  The grid's stream takes the highest priority, whose queues
+// are not shared with normal-priority streams (the library's own and, by
+// default, the caller's); it stays non-blocking, so work on the null stream
+// (torch's default) never waits for the grid either.  (A CU-masked stream
+// would get a queue of its own too, but HIP creates those as blocking
+// streams.)
+hipError_t server_stream_create(hipStream_t *st)
 {
+    int least = 0, greatest = 0;
+    if (g_cfg.serve_prio && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess &&
+        greatest != least)
+        return hipStreamCreateWithPriority(st, hipStreamNonBlocking, greatest);
+    return hipStreamCreateWithFlags(st, hipStreamNonBlocking);
+}
+
+int server_init_locked(Device &D)
+{
+    Server &S = D.srv;
     if (S.ready)
         return WC_OK;
     const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
-    if (hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking) != hipSuccess ||
+    if (server_stream_create(&S.st) != hipSuccess ||
         hipHostMalloc((void **)&S.h_rec, wc::kSrvMaxPkts * sizeof(wc::SrvRec), fl) != hipSuccess ||
         hipHostMalloc((void **)&S.h_res, wc::kSrvMaxPkts * sizeof(wc::SrvRes), fl) != hipSuccess ||
         hipHostMalloc((void **)&S.h_hb, 64, fl) != hipSuccess ||
@@ -1169,7 +1195,7 @@ int serve_batch(Device &D, int dev, const uint8_t *dbase, const uint64_t *h_off,
             ++g_srv_stats.fallbacks;
             return kSrvFallback;
         }
-    int rc = server_init_locked(S);
+    int rc = server_init_locked(D);
     if (rc)
         return rc;
     if (!g_srv_hooks) {
