@@ -122,6 +122,7 @@ struct Device {
     uint32_t rx_words[4] = {}; // tally words launch g % kRxSets may write
     uint32_t rx_gen = 0;
     bool rx_early = false;
+    uint32_t rx_nlaunch[2] = {}, rx_ndecided = 0; // WC_RX_TRACE=2 counts
 };
 constexpr int kRxSets = 4;
 std::mutex g_rx_mu; // rx_launch's tally bookkeeping (batch calls run outside g_mu)
@@ -188,7 +189,9 @@ struct Config {
     int rx_hdrt = 1;               // WC_RX_HDRT: RX verdict header chunks loaded transposed
     int rx_skip = 0;               // WC_RX_SKIP: frames the parse rules out leave the stream
     int rx_adapt = 1;              // WC_RX_ADAPT: EARLY or HT per launch, by the ring's mix
-    int rx_trace = 0;              // WC_RX_TRACE: log each ADAPT decision to stderr (tools)
+    int rx_trace = 0;              // WC_RX_TRACE: log each ADAPT decision to stderr (tools;
+                                   // 2: one summary line per 512 launches)
+    int rx_force = 0;              // WC_RX_FORCE: ADAPT's decision fixed, 1 HT / 2 EARLY (tools)
     int rx_mode() const
     {
         // The default: ADAPT (EARLY or the HT stream per tile, by the share
@@ -331,6 +334,7 @@ void load_config_locked()
     c.rx_skip = env_int("WC_RX_SKIP", c.rx_skip);
     c.rx_adapt = env_int("WC_RX_ADAPT", c.rx_adapt);
     c.rx_trace = env_int("WC_RX_TRACE", c.rx_trace);
+    c.rx_force = env_int("WC_RX_FORCE", c.rx_force);
     {
         std::lock_guard<std::mutex> lk(g_cfg_mu);
         g_cfg = c;
@@ -992,8 +996,19 @@ hipError_t rx_launch(Device &D, const Config &C, const void *base, const uint64_
     // g - 4 after the clear carries g - 4's tag and is not counted)
     memset(D.h_rx_tally[set], 0, words * 4u);
     D.rx_words[set] = words;
+    if (C.rx_force) // (tools: the tallying kernel with the decision fixed)
+        D.rx_early = C.rx_force == 2;
     const int m = wc::kRxHdrT | (D.rx_early ? wc::kRxEarly : 0);
-    if (C.rx_trace)
+    if (C.rx_trace == 2) { // one summary line per 512 launches
+        ++D.rx_nlaunch[D.rx_early ? 1 : 0];
+        D.rx_ndecided += from_words != 0;
+        if ((g & 511u) == 0) {
+            fprintf(stderr, "wccksum rx gen %u: last 512 launches %u HT / %u EARLY, %u decided "
+                            "from an arrived tally\n",
+                    g, D.rx_nlaunch[0], D.rx_nlaunch[1], D.rx_ndecided);
+            D.rx_nlaunch[0] = D.rx_nlaunch[1] = D.rx_ndecided = 0;
+        }
+    } else if (C.rx_trace)
         fprintf(stderr, "wccksum rx gen %u: %s (tally of gen %u: %u words, %u of %u frames ruled "
                         "out; %.1f us on the host)\n",
                 g, D.rx_early ? "EARLY" : "HT", from, from_words, from_out, from_seen,
