@@ -63,7 +63,7 @@ def main():
             buf[sel + 13] = 0x06
         d_off = torch.from_numpy(f_off).to(dev)
         d_len = torch.from_numpy(f_len).to(dev)
-        ip_off = d_off + 14
+        ip_off = torch.from_numpy((f_off + np.uint64(14)).astype(np.uint64)).to(dev)
         ip_len = torch.from_numpy(ip_lens).to(dev)
         out = torch.empty(n, dtype=torch.uint8, device=dev)
         out16 = torch.empty(n, dtype=torch.uint16, device=dev)
