@@ -727,6 +727,21 @@ def traffic_entry(args, meta, path):
         f"FETCH_SIZE x2 + WRITE_SIZE, separate passes; a static lookup, not this run)")
 
 
+_PROBES = {}
+
+
+def _mhz(v: float):
+    return None if v != v else round(v)  # (NaN: no two samples inside the window)
+
+
+def sclk_probe(dev):
+    """One shader-clock probe per device (warpcore_amd.SclkProbe)."""
+    import warpcore_amd as wc
+    if dev not in _PROBES:
+        _PROBES[dev] = wc.SclkProbe(dev)
+    return _PROBES[dev]
+
+
 def measure_leg(args, dev, rank, world, coll_dev, sub, use_graph):
     """One secondary measurement (c3 size, c4, C2 rotating): build the
     workload `sub` (args with its config), warm it, time it on HIP events,
@@ -739,12 +754,17 @@ def measure_leg(args, dev, rank, world, coll_dev, sub, use_graph):
     T.warm(2 * T.per_graph, 0.2)
     steps = T.steps_for(args.extra_seconds)
     wdist.barrier(dev)
+    # the shader clock beside the timed launches (a one-wave probe on its own
+    # stream): clock-sensitive legs (the mixed-size RX ring) move with DVFS
+    probe = sclk_probe(dev)
+    probe.start(0.9 * args.extra_seconds * 1e3)
     ms = wdist.max_over_ranks(T.kernel_ms(steps), coll_dev)
     res = {"kernel_ms_avg_max_rank": round(ms, 5),
            "GBps": round(W.nbytes / (ms * 1e-3) / 1e9, 1),
            "frac": round(W.nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
            "batches": K, "footprint_GB": round(K * W.nbytes / 1e9, 3),
-           "steps": steps, "launch": "hipGraph replay" if T.graph is not None else "stream"}
+           "steps": steps, "launch": "hipGraph replay" if T.graph is not None else "stream",
+           "sclk_MHz": _mhz(probe.mhz())}
     par = parity_check(sub, W)  # every batch's results are from its last timed launch
     res["parity"] = {"checked_packets": wdist.sum_over_ranks(par["checked_packets"], coll_dev),
                      "mismatches": wdist.sum_over_ranks(par["mismatches"], coll_dev)}

@@ -250,6 +250,13 @@ int wc_config_reload(void);
  * word k of [d_buf, d_buf + nbytes) is splitmix64 output k for `seed`. */
 int wc_synth_fill(void *d_buf, uint64_t nbytes, uint64_t seed, void *stream);
 
+/* Shader-clock probe (bench / tools): one wave on `stream` writes n pairs
+ * (100-MHz wall clock, shader clock counter) to d_samples[2 i], [2 i + 1],
+ * one pair every `interval` wall-clock ticks, then ends.  Run beside a
+ * timed workload on another stream; the ratio of successive deltas x 100 is
+ * the shader clock in MHz while it ran. */
+int wc_sclk_probe(uint64_t *d_samples, int n, uint64_t interval, void *stream);
+
 /* Kernel-configuration introspection: fills the group width G (lanes per
  * packet), chunk loads per lane and packets per group-iteration the
  * dispatcher picks for a strided batch of `len`-byte packets. */

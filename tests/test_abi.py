@@ -102,6 +102,11 @@ def test_argument_errors_need_no_gpu():
     # unknown kind (WC_CKSUM_IP = 0, WC_CKSUM_PAYLOAD = 1)
     assert lib.wc_cksum_strided(p, 2048, 64, 8, p, 7, None) == einval
     assert lib.wc_cksum_ragged(p, p, p, 8, p, -1, None) == einval
+    # the shader-clock probe: nothing to do, or no / misaligned sample array
+    assert lib.wc_sclk_probe(None, 0, 2000, None) == ok
+    assert lib.wc_sclk_probe(None, 8, 2000, None) == einval
+    assert lib.wc_sclk_probe(p + 4, 8, 2000, None) == einval
+    assert lib.wc_sclk_probe(p, 8, 0, None) == einval
     assert lib.wc_strerror(einval).decode() == "invalid argument"
 
 

@@ -64,6 +64,10 @@ def test_bench_one_gpu_line(gpu):
     assert rot["batches"] == 4 and rot["parity"] == {"checked_packets": 4 * 65536,
                                                       "mismatches": 0}
     assert line["roofline"]["frac_rotating"] == rot["frac"]
+    # the shader clock sampled beside each secondary leg (wc_sclk_probe)
+    for e in [*c3.values(), c4, rot]:
+        assert e["sclk_MHz"] is None or 300 <= e["sclk_MHz"] <= 3500, e
+    assert c4["sclk_MHz"] is not None
 
 
 def test_bench_c3_rotating_line(gpu):

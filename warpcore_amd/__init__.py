@@ -5,7 +5,7 @@ Product: ``libwccksum.so`` (HIP kernels + C ABI, ``include/warpcore_gpu``).
 This package is the Python host mirror of that C ABI plus the synthetic
 packet generators and the multi-GPU shard driver used by bench.py.
 """
-from .cksum import (KIND_IP, KIND_PAYLOAD, WcError, cksum_host, cksum_host_multi,
+from .cksum import (KIND_IP, KIND_PAYLOAD, SclkProbe, WcError, cksum_host, cksum_host_multi,
                     cksum_ip_udp_host, server_stats,
                     cksum_ip_udp_ragged, cksum_ragged_multi, gather_results_multi,
                     gpu_init_multi, shard_range,
@@ -17,7 +17,7 @@ from .cksum import (KIND_IP, KIND_PAYLOAD, WcError, cksum_host, cksum_host_multi
                     RX_FRAGMENT, RX_BAD_VERSION, RX_NOT_UDP, RX_NOT_IP, RX_TRUNCATED)
 
 __all__ = [
-    "KIND_IP", "KIND_PAYLOAD", "WcError", "cksum_host", "cksum_host_multi",
+    "KIND_IP", "KIND_PAYLOAD", "SclkProbe", "WcError", "cksum_host", "cksum_host_multi",
     "cksum_ip_udp_host", "server_stats",
     "cksum_ip_udp_ragged", "cksum_ragged_multi", "gather_results_multi", "gpu_init_multi",
     "shard_range",

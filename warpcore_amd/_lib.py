@@ -51,6 +51,7 @@ SIGNATURES = {
     "wc_gpu_fini": (_int, []),
     "wc_config_reload": (_int, []),
     "wc_synth_fill": (_int, [_vp, _u64, _u64, _vp]),
+    "wc_sclk_probe": (_int, [_vp, _int, _u64, _vp]),
     "wc_plan_strided": (_int, [_u64, _u64, _u16, _u64, _int,
                                ctypes.POINTER(_int), ctypes.POINTER(_int),
                                ctypes.POINTER(_int), ctypes.POINTER(_int)]),

@@ -470,6 +470,40 @@ def synth_fill(buf: torch.Tensor, seed: int, nbytes: Optional[int] = None,
     return buf
 
 
+class SclkProbe:
+    """The shader clock beside a timed workload (wc_sclk_probe): one wave on
+    a stream of its own samples the 100-MHz wall clock and the shader clock
+    counter every `every_us`.  start() before the timed launches (after the
+    work before them), mhz() after: the median clock over the samples taken.
+    The probe ends by itself after the samples asked for -- keep that inside
+    a timed region that ends with a device-wide synchronisation."""
+
+    def __init__(self, device, max_samples: int = 200000):
+        self.device = torch.device(device)
+        self.max = max_samples
+        self.buf = torch.zeros(2 * max_samples, dtype=torch.int64, device=self.device)
+        self.stream = torch.cuda.Stream(device=self.device)
+        self.n = 0
+
+    def start(self, ms: float, every_us: int = 20) -> None:
+        self.n = int(min(self.max, max(8, ms * 1e3 / every_us)))
+        self.buf.zero_()
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))
+        with _on_device(self.device):
+            _check("wc_sclk_probe", _lib.load().wc_sclk_probe(
+                self.buf.data_ptr(), self.n, every_us * 100, self.stream.cuda_stream))
+
+    def mhz(self) -> float:
+        self.stream.synchronize()
+        s = self.buf[: 2 * self.n].view(self.n, 2).cpu().double()
+        dt = s[1:, 0] - s[:-1, 0]
+        dc = s[1:, 1] - s[:-1, 1]
+        ok = dt > 0
+        if not bool(ok.any()):
+            return float("nan")
+        return float((dc[ok] / dt[ok] * 100.0).median())
+
+
 def plan_strided(base_addr: int, stride: int, length: int, n: int, kind="ip") -> dict:
     vals = [ctypes.c_int() for _ in range(4)]
     _check("wc_plan_strided", _lib.load().wc_plan_strided(

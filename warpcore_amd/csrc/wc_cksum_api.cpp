@@ -2187,6 +2187,20 @@ int wc_config_reload(void)
     return WC_OK;
 }
 
+int wc_sclk_probe(uint64_t *d_samples, int n, uint64_t interval, void *stream)
+{
+    if (n <= 0)
+        return WC_OK;
+    if (!d_samples || !interval || ((uintptr_t)d_samples & 7u))
+        return WC_EINVAL;
+    Device *D = nullptr;
+    Config C;
+    int rc = ensure_device(&D, &C);
+    if (rc)
+        return rc;
+    return hip_err(wc::launch_sclk_probe(d_samples, n, interval, (hipStream_t)stream));
+}
+
 int wc_synth_fill(void *d_buf, uint64_t nbytes, uint64_t seed, void *stream)
 {
     if (!nbytes)

@@ -163,6 +163,7 @@ hipError_t launch_flat(const LaunchArgs &a, int rows, hipStream_t st);
 hipError_t launch_flat_kernel(const LaunchArgs &a, int rows, hipStream_t st);
 hipError_t launch_synth(void *buf, uint64_t nbytes, uint64_t seed, int grid,
                         hipStream_t st);
+hipError_t launch_sclk_probe(uint64_t *out, int n, uint64_t interval, hipStream_t st);
 // RX verdicts of Ethernet frames [base + offs[i], + flens[i]) (wc_k_rx.hip);
 // drops (optional) accumulates the frames the reference's RX path drops.
 // mode: kRxEarly (parse, then stream only the checked frames) | kRxHdrT

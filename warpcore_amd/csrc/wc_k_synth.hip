@@ -1,4 +1,5 @@
-// wc_k_synth.hip -- synthetic payload bytes on the device (bench / tests).
+// wc_k_synth.hip -- synthetic payload bytes on the device (bench / tests),
+// and the shader-clock probe bench.py runs beside its timed legs.
 #include "wc_device.h"
 
 namespace wc {
@@ -40,6 +41,34 @@ k_synth(uint8_t *__restrict__ buf, uint64_t nbytes, uint64_t seed)
 hipError_t launch_synth(void *buf, uint64_t nbytes, uint64_t seed, int grid, hipStream_t st)
 {
     hipLaunchKernelGGL(k_synth, dim3(grid), dim3(256), 0, st, (uint8_t *)buf, nbytes, seed);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Shader-clock probe.  One wave, beside a workload on another stream: lane 0
+// records n pairs (the 100-MHz constant wall clock, the shader clock
+// counter) every `interval` wall ticks; the ratio of successive deltas is
+// the shader clock while the workload ran (DVFS moves it between ~1.5 and
+// ~2.4 GHz on MI355X, and clock-sensitive kernels move with it; DESIGN.md
+// section 5.1).  It always ends after n samples.
+__global__ void __launch_bounds__(64) k_sclk_probe(uint64_t *__restrict__ out, int n,
+                                                   uint64_t interval)
+{
+    if (threadIdx.x != 0)
+        return;
+    for (int i = 0; i < n; ++i) {
+        const uint64_t t0 = wall_clock64();
+        while (wall_clock64() - t0 < interval)
+            __builtin_amdgcn_s_sleep(1);
+        const uint64_t w = wall_clock64(), c = clock64();
+        out[2 * i] = w;
+        out[2 * i + 1] = c;
+    }
+}
+
+hipError_t launch_sclk_probe(uint64_t *out, int n, uint64_t interval, hipStream_t st)
+{
+    hipLaunchKernelGGL(k_sclk_probe, dim3(1), dim3(64), 0, st, out, n, interval);
     return hipGetLastError();
 }
 
