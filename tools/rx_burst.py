@@ -48,6 +48,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--bursts", default="20,200,2000")
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--c4", action="store_true", help="add C4 (2^24 Zipf packed, 4 GB)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     wc.gpu_init(0)
@@ -84,6 +85,19 @@ def main():
 
     cases = [("rx ADAPT", rx, ""), ("rx HT, no tally", rx, "WC_RX_ADAPT=0"),
              ("payload", pay, ""), ("C2", c2fn, "")]
+    if args.c4:  # C4: 2^24 Zipf packets packed (the dense seg path)
+        c4_lens = synth.zipf_lengths(1 << 24)
+        c4_offs = synth.packed_offsets(c4_lens)
+        span = int(c4_lens.astype(np.uint64).sum())
+        c4buf = torch.empty(span + 64, dtype=torch.uint8, device=dev)
+        wc.synth_fill(c4buf, 4, nbytes=span)
+        c4_off = torch.from_numpy(c4_offs).to(dev)
+        c4_len = torch.from_numpy(c4_lens).to(dev)
+        c4out = torch.empty(1 << 24, dtype=torch.uint16, device=dev)
+
+        def c4fn():
+            wc.cksum_ragged(c4buf, c4_off, c4_len, out=c4out, check=False)
+        cases.append(("C4", c4fn, ""))
     bursts = [int(b) for b in args.bursts.split(",")]
     res, clk = {}, {}
 
@@ -102,7 +116,7 @@ def main():
                     fn()
                 torch.cuda.synchronize()
                 time.sleep(0.05)
-                per = 0.12 if name == "C2" else 0.12  # ms, rough
+                per = {"C2": 0.21, "C4": 0.62}.get(name, 0.12)  # ms per launch, rough
                 ns = int(min(200000, b * per * 1e3 / 20 + 100))
                 samples.zero_()
                 torch.cuda.synchronize()
