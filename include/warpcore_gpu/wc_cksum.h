@@ -238,7 +238,9 @@ int wc_gather_results_multi(uint16_t *const *d_shard_out, const uint64_t *n,
 int wc_gpu_init(int device);
 /* Release the scratch created by wc_gpu_init / wc_gpu_init_multi and the
  * RCCL communicators.  Page-locks taken with wc_host_register are the
- * caller's and stay until wc_host_unregister. */
+ * caller's and stay until wc_host_unregister.  Every other entry point may
+ * be called from any thread at any time, but not while wc_gpu_fini runs:
+ * the caller quiesces its engine threads first. */
 int wc_gpu_fini(void);
 
 /* The WC_* tuning environment (kernel shapes, path choices) is
