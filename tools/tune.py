@@ -188,7 +188,7 @@ def main():
              "WC_DIAG_NOLOAD", "WC_FLAT_MIN", "WC_RAGGED_SHAPE", "WC_VARIANT", "WC_SEG",
              "WC_SEG_ROWS", "WC_GRP_DENSE", "WC_GRP_SPARSE", "WC_GRP_ROWS",
              "WC_STRIDED_SEG", "WC_FLAT_PK", "WC_GATHER", "WC_RX_EARLY", "WC_RX_HDRT", "WC_RX_SKIP",
-             "WC_RX_ADAPT", "WC_LEAN_PHASE", "WC_SPLIT_PKTS", "WC_SPLIT_BYTES"}
+             "WC_RX_ADAPT", "WC_RX_GRID", "WC_RX_FORCE", "WC_LEAN_PHASE", "WC_SPLIT_PKTS", "WC_SPLIT_BYTES"}
     knobs |= {kv.split("=", 1)[0] for v in variants for kv in v.split()}
     knobs |= {k for k in os.environ if k.startswith("WC_") and k != "WC_NO_BUILD"}
     base_env = {k: os.environ.get(k) for k in knobs}

@@ -192,6 +192,7 @@ struct Config {
     int rx_trace = 0;              // WC_RX_TRACE: log each ADAPT decision to stderr (tools;
                                    // 2: one summary line per 512 launches)
     int rx_force = 0;              // WC_RX_FORCE: ADAPT's decision fixed, 1 HT / 2 EARLY (tools)
+    int rx_grid = 0;               // WC_RX_GRID: cap the RX grid at this many blocks (tools)
     int rx_mode() const
     {
         // The default: ADAPT (EARLY or the HT stream per tile, by the share
@@ -335,6 +336,7 @@ void load_config_locked()
     c.rx_adapt = env_int("WC_RX_ADAPT", c.rx_adapt);
     c.rx_trace = env_int("WC_RX_TRACE", c.rx_trace);
     c.rx_force = env_int("WC_RX_FORCE", c.rx_force);
+    c.rx_grid = std::max(0, env_int("WC_RX_GRID", c.rx_grid));
     {
         std::lock_guard<std::mutex> lk(g_cfg_mu);
         g_cfg = c;
@@ -961,7 +963,8 @@ hipError_t rx_launch(Device &D, const Config &C, const void *base, const uint64_
 {
     const int mode = C.rx_mode();
     if (!(mode & wc::kRxAdapt) || !D.h_rx_tally[0])
-        return wc::launch_rx_verdict(base, offs, flens, n, verdict, drops, C.nt != 0, st, mode);
+        return wc::launch_rx_verdict(base, offs, flens, n, verdict, drops, C.nt != 0, st, mode,
+                                     nullptr, 0u, C.rx_grid);
     std::lock_guard<std::mutex> lk(g_rx_mu);
     const auto t0 = std::chrono::steady_clock::now();
     uint32_t from = 0, from_words = 0, from_seen = 0, from_out = 0;
@@ -1015,7 +1018,7 @@ hipError_t rx_launch(Device &D, const Config &C, const void *base, const uint64_
                 std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0)
                     .count());
     return wc::launch_rx_verdict(base, offs, flens, n, verdict, drops, C.nt != 0, st, m,
-                                 D.d_rx_tally[set], g & 0xFFFFu);
+                                 D.d_rx_tally[set], g & 0xFFFFu, C.rx_grid);
 }
 
 // One device launch over a ragged batch of `kind` (a checksum kind, RX

@@ -177,7 +177,7 @@ constexpr uint32_t kRxTallyWords = 1024;
 hipError_t launch_rx_verdict(const void *base, const uint64_t *offs, const uint16_t *flens,
                              uint64_t n, uint8_t *verdict, uint64_t *drops, bool nt,
                              hipStream_t st, int mode = 0, uint32_t *tally = nullptr,
-                             uint32_t gen = 0);
+                             uint32_t gen = 0, int max_grid = 0);
 
 // Resident small-batch server (wc_k_serve.hip).  Host-mapped pinned memory:
 // one record per packet, written by the host (seq last), polled / read by the

@@ -448,11 +448,16 @@ static hipError_t launch_rx_one(const void *base, const uint64_t *offs, const ui
 
 hipError_t launch_rx_verdict(const void *base, const uint64_t *offs, const uint16_t *flens,
                              uint64_t n, uint8_t *verdict, uint64_t *drops, bool nt,
-                             hipStream_t st, int mode, uint32_t *tally, uint32_t gen)
+                             hipStream_t st, int mode, uint32_t *tally, uint32_t gen,
+                             int max_grid)
 {
     const uint64_t tiles = (n + 63) / 64;
+    // One tile per wave (one-shot); max_grid > 0 (WC_RX_GRID, tools) caps the
+    // grid, each wave then walks several tiles with the next tile's metadata
+    // prefetched.
+    const uint64_t cap = max_grid > 0 ? (uint64_t)max_grid : kMaxGridBlocks;
     const int grid = (int)std::min<uint64_t>(
-        kMaxGridBlocks, std::max<uint64_t>(1, (tiles + kFlatWaves - 1) / kFlatWaves));
+        cap, std::max<uint64_t>(1, (tiles + kFlatWaves - 1) / kFlatWaves));
     // EARLY streams only the checked frames: SKIP has nothing to skip there,
     // and is dropped so that NT and HDRT are still honoured.
     const bool early = mode & kRxEarly, ht = mode & kRxHdrT, skip = (mode & kRxSkip) && !early;
