@@ -218,15 +218,26 @@ __device__ __forceinline__ RxParse rx_parse(const u32x4 (&c)[5], uint64_t fa, ui
     const u32x4 xu = ju <= 2u ? c[2] : (ju == 3u ? c[3] : c[4]);
     const u32x4 yu = ju <= 2u ? c[3] : (ju == 3u ? c[4] : z4);
     const uint32_t g0 = win_bytes(xu, yu, yu, u & 15u, 0);
-    // ip_cksum(ip, hl) (ip4.c:110-115) over frame bytes [14, 14 + hl), as in
-    // rx_parse_slow; 14 + 40 + 15 < 80: inside the five chunks.
+    // ip_cksum(ip, hl) (ip4.c:110-115) over frame bytes [14, 14 + hl),
+    // 20 <= hl <= 40 here (14 + 40 + 15 < 80: inside the five chunks): the
+    // header's little-endian words summed header-relative, as csum_oc16 reads
+    // them (in_cksum.c:107-120) -- two 20-byte windows rotated out of the
+    // chunks, one dot2 per dword, so no address-parity fix.  (Per-chunk byte
+    // masks over all five chunks took about twice the VALU.)
+    const uint32_t o = sf + 14u;  // header start in the chunk stream: 14..29
+    const uint32_t o2 = o + 20u;  // its second 20 bytes: 34..49
+    const bool j0 = o >= 16u, j2 = o2 >= 48u;
+    uint32_t h0[5], h1[5];
+    win_rot(j0 ? c[1] : c[0], j0 ? c[2] : c[1], j0 ? c[3] : c[2], o & 15u, h0);
+    win_rot(j2 ? c[3] : c[2], j2 ? c[4] : c[3], j2 ? z4 : c[4], o2 & 15u, h1);
     uint32_t V = 0;
-    if (x.v4 && x.hdr_in) {
 #pragma unroll
-        for (int k = 0; k < 5; ++k)
-            V += seg_range(c[k], 16 * k - (int)(sf + 14u), 0, (int)min(x.hl, 40u));
-    }
-    const uint16_t ipck = fold_not(((fa + 14u) & 1u) ? __builtin_amdgcn_alignbit(V, V, 24) : V);
+    for (int m = 0; m < 5; ++m)
+        V = wsum(h0[m], V);
+#pragma unroll
+    for (int m = 0; m < 5; ++m) // header bytes 20 + 4 m .. 23 + 4 m, if below hl
+        V = wsum(x.hl > 20u + 4u * m ? h1[m] : 0u, V);
+    const uint16_t ipck = fold_not(V);
     return rx_decide(fa, flen, valid, x, g0, ipck);
 }
 
