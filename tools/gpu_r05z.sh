@@ -5,7 +5,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 REPO=$PWD
-OUT=$REPO/gpurun_out/r05z
+OUT=$REPO/gpurun_out/${TAG:-r05z}
 mkdir -p $OUT
 export TMPDIR=/tmp WC_NO_BUILD=1
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
