@@ -1,10 +1,10 @@
 #!/usr/bin/env bash
-# Round 5, call aa: the RX parse's IPv4 header sum from two rotated 20-byte
+# Round 5, call aa / af: RX parse changes -- RX parity in every mode, then the rings timed.
 # windows (half the VALU of per-chunk byte masks) -- RX parity in every mode,
 # then the rings timed (compare call y's defaults: 112.8 / 97.1 / 236.3 us).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=gpurun_out/r05aa
+OUT=gpurun_out/${TAG:-r05aa}
 mkdir -p $OUT
 export TMPDIR=/tmp WC_NO_BUILD=1
 timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_rx.py \

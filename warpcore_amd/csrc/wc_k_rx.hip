@@ -167,17 +167,27 @@ __device__ __forceinline__ void rx_load(uint64_t fa, uint32_t flen, bool valid, 
 // is loaded per lane, and only by lanes whose start phase sf > 2 may need it
 // (the parse reads frame bytes < 14 + 40 + 8 = 62).  rx_hdr_gather then hands
 // each lane its frame's chunks through LDS.
+// Each lane finds its frame's address and length in a 1-KB LDS table the
+// tile's lanes write first (one 16-byte store, four 16-byte reads, all
+// issued back to back), not by twelve cross-lane shuffles, each a dependent
+// LDS round trip before the next header load.  `tbl` is the tile's
+// descriptor table, which flat_tile_setup rewrites afterwards.
 __device__ __forceinline__ void rx_load_t(uint64_t fa, uint32_t flen, bool valid, uint64_t zero,
-                                          int lane, u32x4 (&hx)[4], u32x4 &c4)
+                                          int lane, u32x4 *tbl, u32x4 (&hx)[4], u32x4 &c4)
 {
     const uint32_t lv = valid ? flen : 0u;
+    tbl[lane] = u32x4{(uint32_t)fa, (uint32_t)(fa >> 32), lv, 0u};
+    wave_order();
+    u32x4 e[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        e[i] = tbl[16 * i + (lane >> 2)]; // frame 16 i + lane / 4
+    wave_order(); // (the table is rewritten by flat_tile_setup)
     const uint64_t j16 = 16ull * (uint32_t)(lane & 3);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const int f = 16 * i + (lane >> 2);
-        const uint64_t faf = (uint64_t)(uint32_t)__shfl((int)(uint32_t)fa, f, 64) |
-                             ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(fa >> 32), f, 64) << 32);
-        const uint32_t lf = (uint32_t)__shfl((int)lv, f, 64);
+        const uint64_t faf = (uint64_t)e[i].x | ((uint64_t)e[i].y << 32);
+        const uint32_t lf = e[i].z;
         const uint64_t a = (faf & ~15ull) + j16;
         hx[i] = load_chunk<false>(lf != 0u && a < faf + lf ? a : zero);
     }
@@ -345,7 +355,7 @@ k_rx_verdict(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
         u32x4 c[5];
         u32x4 hx[4], c4;
         if constexpr (HT)
-            rx_load_t(fa, flen, valid, zero, lane, hx, c4);
+            rx_load_t(fa, flen, valid, zero, lane, reinterpret_cast<u32x4 *>(L.f.desc), hx, c4);
         else
             rx_load(fa, flen, valid, zero, c);
         auto headers = [&] { // this lane's frame chunks 0..4 (HT: through LDS)
