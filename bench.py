@@ -48,6 +48,7 @@ from __future__ import annotations
 
 import argparse
 import copy
+import gc
 import json
 import os
 import sys
@@ -111,6 +112,9 @@ def parse(argv=None):
     ap.add_argument("--no-rings", action="store_true",
                     help="skip the netmap RX-ring legs (rx, zrx, zrx with ARP) of the default line")
     ap.add_argument("--c3-packets", type=int, default=1 << 20, help="packets per c3 size")
+    ap.add_argument("--ring-packets", type=int, default=1 << 20,
+                    help="frames of the MTU ring leg (the mixed-size ring legs: twice as "
+                         "many at the default)")
     ap.add_argument("--c4-packets", type=int, default=1 << 24, help="packets of the c4 object")
     ap.add_argument("--extra-seconds", type=float, default=0.25,
                     help="timed seconds per c3 / c4 / frac_rotating measurement")
@@ -122,6 +126,11 @@ def parse(argv=None):
                     help="keep warming up (untimed) until this long has passed, so the "
                          "GPU clock has ramped from idle before the timed steps")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="skip the end-to-end (host memory in and out) object")
+    ap.add_argument("--e2e-packets", type=int, default=1 << 20,
+                    help="packets per rank of each end-to-end call")
+    ap.add_argument("--e2e-reps", type=int, default=3, help="timed calls per e2e case")
     ap.add_argument("--traffic-file", default=str(ROOT / "profiles" / "traffic.json"))
     return ap.parse_args(argv)
 
@@ -423,13 +432,17 @@ class Timer:
     rotations) -- the graph takes the Python launch cost out of small-batch
     timings (a 64-B C3 kernel is ~9 us, a Python launch about as long)."""
 
-    def __init__(self, W, dev, use_graph: bool, rotate: int = 1, min_graph_steps: int = 8):
+    def __init__(self, W, dev, use_graph: bool, rotate: int = 1, min_graph_steps: int = 8,
+                 exact_steps: int = 0):
         self.W, self.dev = W, dev
         self.graph = None
         self.per_graph = 1
         if use_graph:
             K = max(1, rotate)
-            self.per_graph = K * max(1, -(-min_graph_steps // K))
+            # exact_steps: the graph holds exactly that many steps (the
+            # headline's K timed launches, one replay); else a whole number
+            # of rotations of at least min_graph_steps
+            self.per_graph = exact_steps or K * max(1, -(-min_graph_steps // K))
             torch.cuda.synchronize(dev)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
@@ -702,6 +715,150 @@ def c5_leg(args, dev, rank, world, coll_dev):
     }
 
 
+def _host_ring(dev, n, ip_len, seed, slot=2048):
+    """A netmap ring of n well-formed UDP frames (2:1 IPv4 / IPv6, valid
+    header and UDP checksums; synth.make_rx_ring) of `ip_len`-byte IP packets
+    in `slot`-byte buffers, built on the device and copied to host memory
+    twice: as the RX ring (checksums stored) and as the TX queue (both
+    checksum fields 0, as mk_ip4_hdr / udp_tx leave them before the
+    checksums are computed, ip4.c:184-186, udp.c:209-213).
+    Returns (rx bytes, tx bytes, frame offsets, frame lengths)."""
+    import warpcore_amd as wc
+    from warpcore_amd import synth
+    d = torch.empty(n * slot + 64, dtype=torch.uint8, device=dev)
+    wc.synth_fill(d, seed, nbytes=n * slot)
+    f_off, f_len = synth.make_rx_ring(d, n, np.full(n, ip_len, dtype=np.uint16), slot=slot)
+    rx = d.cpu().numpy()
+    ip = torch.from_numpy(f_off.astype(np.int64)).to(dev) + 14
+    v6 = (torch.arange(n, device=dev) % 3) == 0  # make_rx_ring's v6_every
+    for at4, at6 in ((10, None), (11, None), (26, 46), (27, 47)):
+        d[ip[~v6] + at4] = 0
+        if at6 is not None:
+            d[ip[v6] + at6] = 0
+    tx = d.cpu().numpy()
+    del d, ip, v6
+    return rx, tx, f_off, f_len
+
+
+def e2e_leg(args, dev, rank, world, coll_dev):
+    """North star: "this path starts and ends in host memory (netmap rings or
+    socket buffers), so the end-to-end rate including pinned hipMemcpyAsync in
+    and out must also be measured".  The three host-memory calls the hooks
+    make, each over 2^20 packets of C2's 1472 B, in
+    a registered (page-locked: wc_host_register, netmap's w->mem) and in a
+    pageable host region:
+      * wc_cksum_host        -- C2's strided bytes, ip_cksum;
+      * wc_cksum_ip_udp_host -- the TX batch point (backend_netmap.c:348-358):
+                                well-formed IPv4 / IPv6 UDP packets at +14 of
+                                2048-B slots, both checksum fields 0;
+      * wc_rx_verdict_host   -- the RX batch point (backend_netmap.c:379-391):
+                                the same frames as a ring, checksums stored.
+    Every call is timed from host memory in to host results out (one
+    synchronous call: pipelined H2D, kernel, D2H), beside the measured
+    hipMemcpy H2D ceiling of the same bytes (torch copy_ from pinned and from
+    pageable memory).  Every result is checked against the oracle.  At N > 1
+    every rank runs its own batch over its own link at the same time (barrier
+    before each timed call), so GBps is the whole node's rate: N x bytes over
+    the slowest rank's time."""
+    import warpcore_amd as wc
+    from oracle import c_oracle  # checker only
+    from warpcore_amd import dist as wdist
+    from warpcore_amd import synth
+
+    n, L, reps = args.e2e_packets, 1472, max(1, args.e2e_reps)
+    seed = synth.SEED + 0xE2E + rank
+    d = torch.empty(n * L + 64, dtype=torch.uint8, device=dev)
+    wc.synth_fill(d, seed, nbytes=n * L)
+    c2 = d[: n * L].cpu().numpy()
+    rx, tx, f_off, f_len = _host_ring(dev, n, L, seed + 1)
+    ip_off = f_off + np.uint64(14)
+    ip_len = (f_len.astype(np.int64) - 14).astype(np.uint16)
+
+    def timed(fn):
+        """best and median seconds of `reps` calls, each bracketed by a
+        barrier; the slowest rank's."""
+        ts = []
+        for _ in range(reps):
+            wdist.barrier(dev)
+            t0 = time.perf_counter()
+            fn()
+            ts.append(wdist.max_over_ranks(time.perf_counter() - t0, coll_dev))
+        return min(ts), sorted(ts)[len(ts) // 2]
+
+    # the copy ceiling: the same C2 bytes host -> device (hipMemcpyAsync)
+    pinned = torch.empty(n * L, dtype=torch.uint8, pin_memory=True)
+    pinned.copy_(torch.from_numpy(c2))
+    pageable = torch.from_numpy(c2)
+    ceiling = {}
+    for name, src in (("pinned", pinned), ("pageable", pageable)):
+        def copy(src=src):
+            d[: n * L].copy_(src, non_blocking=True)
+            torch.cuda.synchronize(dev)
+        copy()
+        best, _ = timed(copy)
+        ceiling[name] = round(world * n * L / best / 1e9, 2)
+    del pinned, pageable, d
+    torch.cuda.empty_cache()
+
+    # every call's expected results (oracle on the same host bytes)
+    c2_off = np.arange(n, dtype=np.uint64) * np.uint64(L)
+    c2_len = np.full(n, L, dtype=np.uint16)
+    want_c2 = c_oracle.cksum_strided(c2, L, L, n, kind=0)
+    want_pay = c_oracle.cksum_ragged(tx, ip_off, ip_len, kind=1)
+    b0 = tx[ip_off.astype(np.int64)]
+    v4 = (b0 >> 4) == 4
+    hl = np.where(v4, (b0 & 0x0F).astype(np.uint16) * 4, 0).astype(np.uint16)
+    want_hdr = np.where(v4, c_oracle.cksum_ragged(tx, ip_off, hl, kind=0), 0).astype(np.uint16)
+    want_rx = c_oracle.rx_verdict_ragged(rx, f_off, f_len)
+
+    calls = {
+        "cksum_host": (c2, lambda: wc.cksum_host(c2, c2_off, c2_len, kind="ip"),
+                       lambda got: int((got != want_c2).sum()), n * L),
+        "cksum_ip_udp_host": (tx, lambda: wc.cksum_ip_udp_host(tx, ip_off, ip_len),
+                              lambda got: int((got[0] != want_hdr).sum() +
+                                              (got[1] != want_pay).sum()),
+                              int(ip_len.astype(np.uint64).sum())),
+        "rx_verdict_host": (rx, lambda: wc.rx_verdict_host(rx, f_off, f_len),
+                            lambda got: int((got[0] != want_rx).sum()),
+                            int(f_len.astype(np.uint64).sum())),
+    }
+    res = {}
+    for name, (region, fn, bad_of, nbytes) in calls.items():
+        res[name] = {"bytes_per_rank": nbytes}
+        for kind in ("registered", "pageable"):
+            if kind == "registered":
+                wc.host_register(region)
+            try:
+                bad = bad_of(fn())  # warm-up call, checked
+                best, med = timed(fn)
+                bad += bad_of(fn())  # and the results of a timed-state call
+            finally:
+                if kind == "registered":
+                    wc.host_unregister(region)
+            gbps = world * nbytes / best / 1e9
+            res[name][kind] = {
+                "GBps": round(gbps, 2), "GBps_median": round(world * nbytes / med / 1e9, 2),
+                "ms_best": round(best * 1e3, 3),
+                "frac_of_h2d_pinned": round(gbps / ceiling["pinned"], 4),
+                "parity": {"checked_packets": wdist.sum_over_ranks(2 * n, coll_dev),
+                           "mismatches": wdist.sum_over_ranks(bad, coll_dev)}}
+    rx_ok = int(np.isin(want_rx, (0, 1)).sum())
+    return {
+        "workload": (f"{n} packets x {L} B per rank from host memory to host results, one "
+                     f"synchronous call each (pipelined hipMemcpyAsync H2D, kernel, D2H of the "
+                     f"results): wc_cksum_host over C2's strided bytes; wc_cksum_ip_udp_host "
+                     f"(TX) and wc_rx_verdict_host (RX) over the same {L}-B UDP/IP packets "
+                     f"(2:1 IPv4/IPv6) in 2048-B netmap slots ({L + 14}-B frames); registered "
+                     f"(page-locked) and pageable regions; {world} rank(s) at once, each over "
+                     f"its own link; best of {reps}"),
+        "n_ranks": world,
+        "h2d_ceiling_GBps": {**ceiling, "how": "torch copy_ of the C2 bytes to the device "
+                                              "(hipMemcpyAsync H2D), best of %d" % reps},
+        "calls": res,
+        "rx_frames_ok": wdist.sum_over_ranks(rx_ok, coll_dev),
+    }
+
+
 def traffic_entry(args, meta, path):
     """HBM bytes per launch for this workload from profiles/traffic.json
     (PMC FETCH_SIZE x2 + WRITE_SIZE, separate rocprofv3 passes): (bytes,
@@ -820,7 +977,7 @@ def extra_legs(args, dev, rank, world, coll_dev):
                               "every verdict checked against oracle_rx_verdict")}
         for name, cfg, arp in (("rx_mtu", "rx", 0), ("zrx", "zrx", 0), ("zrx_arp3", "zrx", 3)):
             sub = copy.copy(base)
-            sub.config, sub.packets, sub.len, sub.rx_arp = cfg, 1 << 20, 1472, arp
+            sub.config, sub.packets, sub.len, sub.rx_arp = cfg, args.ring_packets, 1472, arp
             rings[name] = measure_leg(args, dev, rank, world, coll_dev, sub, use_graph=False)
     return c2rot, c3, c4, rings
 
@@ -841,8 +998,13 @@ def main():
     W = make_workload(args, dev, rank, world)
     n, nbytes, meta = W.n, W.nbytes, W.meta
     K = len(W.batches)
-    use_graph = args.graph == "on" or (args.graph == "auto" and args.config == "c3")
-    T = Timer(W, dev, use_graph, rotate=K)
+    # The timed launches replay from a hipGraph for c2 (all K timed steps
+    # captured once: one replay, no Python launch cost between t0 and the
+    # first kernel -- VERDICT r05 item 4, tools/diag_headline.py) and c3 (a
+    # whole number of rotations per graph: a 64-B batch's kernel is ~9 us).
+    use_graph = args.graph == "on" or (args.graph == "auto" and args.config in ("c2", "c3"))
+    T = Timer(W, dev, use_graph, rotate=K,
+              exact_steps=args.steps if args.config == "c2" else 0)
     T.warm(args.warmup, args.warmup_seconds)
     wdist.barrier(dev)
 
@@ -850,12 +1012,14 @@ def main():
     stream = torch.cuda.current_stream(dev)  # the stream every launch goes to
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
+    gc.disable()  # (no collector pass inside the timed region)
     t0 = time.perf_counter()
     ev0.record(stream)
     T.run(steps)
     ev1.record(stream)
     wdist.barrier(dev)
     elapsed = time.perf_counter() - t0
+    gc.enable()
     kernel_ms = ev0.elapsed_time(ev1) / steps
 
     elapsed = wdist.max_over_ranks(elapsed, coll_dev)
@@ -926,6 +1090,9 @@ def main():
     c5 = None
     if not args.no_c5 and args.config != "c5":
         c5 = c5_leg(args, dev, rank, world, coll_dev)
+    e2e = None
+    if not args.no_e2e and args.config == "c2" and not args.fused and args.kind == "ip":
+        e2e = e2e_leg(args, dev, rank, world, coll_dev)
 
     if rank == 0:
         roof = {"bound": "hbm", "achieved": round(achieved, 1),
@@ -935,7 +1102,10 @@ def main():
                 "frac_job": round(frac_job, 4),
                 "kernel_ms_avg": round(kernel_ms, 5),
                 "kernel_ms_avg_max_rank": round(kernel_ms_max, 5),
-                "timing": "hipGraph replay" if use_graph else "stream launches"}
+                "timing": ((f"hipGraph replay ({T.per_graph} launches per graph)"
+                            if use_graph else "stream launches")
+                           + "; whole-job time from barrier + synchronize to barrier + "
+                             "synchronize, kernel time from HIP events on the launch stream")}
         if frac_l3 is not None:
             roof["frac_l3_resident"] = frac_l3
         if c2rot is not None:
@@ -970,6 +1140,8 @@ def main():
             line["c4"] = c4
         if rings is not None:
             line["rings"] = rings
+        if e2e is not None:
+            line["e2e"] = e2e
         if gather is not None:
             line["results_allgather"] = gather
         print(json.dumps(line), flush=True)

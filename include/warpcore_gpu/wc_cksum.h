@@ -156,7 +156,11 @@ int wc_cksum_host(const void *h_base, uint64_t h_bytes, const uint64_t *h_off,
  * raw.  Same paths and rules as wc_cksum_host: a small registered batch is
  * answered by the resident server or one zero-copy launch, anything else is
  * pipelined.  An IPv4 header (hl bytes, options included) must lie inside
- * [h_base, h_base + h_bytes) even where len is shorter.  Synchronous. */
+ * [h_base, h_base + h_bytes) even where len is shorter: its checksum is
+ * defined whatever len is, and every path reads it whole.  len < hl itself is
+ * outside payload_cksum's defined inputs (the reference's len - hl wraps to
+ * ~4 GiB, in_cksum.c:164): h_out_payload is then unspecified (no byte past
+ * the packet's span is read).  Synchronous. */
 int wc_cksum_ip_udp_host(const void *h_base, uint64_t h_bytes, const uint64_t *h_off,
                          const uint16_t *h_len, uint64_t n, uint16_t *h_out_ip_hdr,
                          uint16_t *h_out_payload);
@@ -166,6 +170,19 @@ int wc_cksum_ip_udp_host(const void *h_base, uint64_t h_bytes, const uint64_t *h
  * asked for but could not answer (they took the launch path instead), and
  * grid launches. */
 int wc_server_stats(uint64_t *served, uint64_t *fallbacks, uint64_t *launches);
+
+/* Quiesce the resident server.  While its grid is resident (it stays up while
+ * small registered calls keep coming, and for WC_SERVE_IDLE_US -- 20 ms --
+ * after the last), a device-wide synchronisation in the same process
+ * (hipDeviceSynchronize, torch.cuda.synchronize()) waits for it: under steady
+ * small-batch traffic, with no end.  wc_server_pause stops the grid on every
+ * device and returns once no wave of it is left; until the matching
+ * wc_server_resume, small registered batches take the zero-copy launch
+ * instead (the same results, ~10 us more per call).  Pauses nest: the server
+ * serves again after as many resumes as pauses.  wc_server_resume without a
+ * pause is WC_EINVAL.  Callable from any thread. */
+int wc_server_pause(void);
+int wc_server_resume(void);
 
 /* Page-lock a host region (e.g. the netmap buffer area w->mem,
  * backend_netmap.c:149-151) so wc_cksum_host can DMA from it directly.

@@ -32,10 +32,14 @@ def gpu():
 
 @pytest.fixture(autouse=True)
 def _fresh_wc_config():
-    """libwccksum reads its WC_* tuning environment once; a test that
-    monkeypatches it calls wc.reload_config(), and every test starts from the
-    (restored) environment of the session."""
+    """libwccksum reads its WC_* environment once; a test that monkeypatches
+    it calls wc.reload_config() (which also moves the mirror's calls to the
+    tuning build while a path knob is set: only that build reads them), and
+    every test starts from the (restored) environment of the session, on the
+    shipped library."""
     from warpcore_amd import _lib
     if _lib._lib is not None:
-        _lib._lib.wc_config_reload()
+        for lib in {id(x): x for x in (_lib._lib, _lib._tune) if x is not None}.values():
+            lib.wc_config_reload()
+        _lib.select_for_env()
     yield

@@ -62,11 +62,44 @@ def test_production_library_has_no_tuning_paths():
     flat = re.findall(r"wc::k_cksum_flat<(\d+), (\d+), (\w+), (\w+), (\w+), (\d+)>", syms)
     assert flat and not any(noload == "true" for *_, noload, _pk in flat)
     assert "TUNING" not in _lib.load().wc_version().decode()
-    text = (ROOT / "warpcore_amd" / "csrc" / "wc_cksum_api.cpp").read_text()
+    text = (ROOT / "warpcore_amd" / "csrc" / "wc_rt_config.cpp").read_text()
     # the env reads of both knobs sit inside #ifdef WC_TUNING
     block = text[text.index("#ifdef WC_TUNING"):text.index("#endif", text.index("#ifdef WC_TUNING"))]
     assert '"WC_VARIANT"' in block and '"WC_DIAG_NOLOAD"' in block
     assert text.count('"WC_VARIANT"') == 1 and text.count('"WC_DIAG_NOLOAD"') == 1
+
+
+def _env_reads_outside_tuning(text: str) -> set:
+    """WC_* names a source reads from the environment outside its
+    #ifdef WC_TUNING ... #endif blocks."""
+    out = re.sub(r"#ifdef WC_TUNING.*?#endif", "", text, flags=re.S)
+    return set(re.findall(r'(?:env_int|env_u64|getenv|parse_shape\(getenv)\("(WC_[A-Z_]+)"', out))
+
+
+def test_production_library_reads_only_integrator_knobs():
+    """The shipped library's paths are a compile-time table: outside the
+    tuning build it reads only the server's sizing / lifetime and the
+    staging pool's width from the environment."""
+    reads = set()
+    for src in sorted((ROOT / "warpcore_amd" / "csrc").glob("wc_rt*.cpp")):
+        reads |= _env_reads_outside_tuning(src.read_text())
+    assert reads == set(_lib.INTEGRATOR_KNOBS), reads
+
+
+def test_path_knobs_select_the_tuning_build(monkeypatch):
+    """warpcore_amd.reload_config() sends the mirror's calls to the tuning
+    build while a path knob is set (only it reads them), and back to the
+    shipped library once none is."""
+    for k in _lib.tuning_knobs():
+        monkeypatch.delenv(k)
+    assert not _lib.is_tuning(_lib.select_for_env())
+    monkeypatch.setenv("WC_SHAPE", "32,4,1")
+    monkeypatch.setenv("WC_SERVE_IDLE_US", "5000")  # an integrator knob: not a path knob
+    assert _lib.tuning_knobs() == ["WC_SHAPE"]
+    assert _lib.is_tuning(_lib.select_for_env())
+    monkeypatch.delenv("WC_SHAPE")
+    assert not _lib.is_tuning(_lib.select_for_env())
+    assert _lib.active() is _lib.load()
 
 
 def test_build_staleness_is_a_source_hash():

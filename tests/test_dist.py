@@ -1,4 +1,4 @@
-"""Multi-process (gloo, world size 2, CPU) tests of the packet sharding used by
+"""Multi-process (gloo, world sizes 2, 4 and 8, CPU) tests of the packet sharding used by
 bench.py --gpus N: even contiguous shards, no data-path collective, results
 gathered in packet order afterwards.  On CPU the per-rank compute is the
 oracle (test infrastructure); on the GPU box it is libwccksum."""
@@ -60,11 +60,13 @@ def _worker(rank, world, port, n, L, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n", [1001, 4096])
-def test_gloo_world2_sharded_equals_whole_batch(n):
+@pytest.mark.parametrize("world,n", [(2, 1001), (2, 4096), (4, 1001), (8, 1001), (8, 4099)])
+def test_gloo_sharded_equals_whole_batch(world, n):
+    """World sizes 2, 4 and 8 (the driver's 8-GPU run, rehearsed on gloo):
+    uneven shards, the padded all-gather back in packet order, max and sum
+    over the ranks."""
     from oracle import c_oracle
     L = 1472
-    world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()

@@ -27,7 +27,23 @@ SMALL_C5 = ["--total-packets", str(1 << 22), "--window-packets", str(1 << 20)]
 
 
 SMALL_EXTRA = ["--c3-packets", "65536", "--c4-packets", "200000", "--rotate-bytes",
-               str(64 << 20), "--extra-seconds", "0.05"]
+               str(64 << 20), "--extra-seconds", "0.05", "--e2e-packets", "65536",
+               "--e2e-reps", "2", "--ring-packets", "65536"]
+E2E_CALLS = ("cksum_host", "cksum_ip_udp_host", "rx_verdict_host")
+
+
+def check_e2e(e2e: dict, ranks: int, n: int = 65536) -> None:
+    """The end-to-end object: three host-memory calls x two memory kinds, a
+    positive rate against a positive H2D ceiling, every result exact."""
+    assert e2e["n_ranks"] == ranks
+    assert e2e["h2d_ceiling_GBps"]["pinned"] > 0 and e2e["h2d_ceiling_GBps"]["pageable"] > 0
+    assert set(e2e["calls"]) == set(E2E_CALLS)
+    for name in E2E_CALLS:
+        for kind in ("registered", "pageable"):
+            c = e2e["calls"][name][kind]
+            assert c["GBps"] > 0 and 0 < c["frac_of_h2d_pinned"] < 2, (name, kind, c)
+            assert c["parity"] == {"checked_packets": ranks * 2 * n, "mismatches": 0}, (name, kind)
+    assert e2e["rx_frames_ok"] == ranks * n
 
 
 def test_bench_one_gpu_line(gpu):
@@ -68,6 +84,7 @@ def test_bench_one_gpu_line(gpu):
     for e in [*c3.values(), c4, rot]:
         assert e["sclk_MHz"] is None or 300 <= e["sclk_MHz"] <= 3500, e
     assert c4["sclk_MHz"] is not None
+    check_e2e(line["e2e"], 1)
 
 
 def test_bench_c3_rotating_line(gpu):
@@ -82,7 +99,7 @@ def test_bench_c3_rotating_line(gpu):
     line = _last_json(r.stdout)
     assert line["config"]["batches"] == 4 and line["steps"] % 8 == 0
     assert line["parity"] == {"checked_packets": 4 * 65536, "mismatches": 0}
-    assert line["roofline"]["timing"] == "hipGraph replay"
+    assert line["roofline"]["timing"].startswith("hipGraph replay (8 launches per graph)")
     assert 0 < line["roofline"]["frac_l3_resident"] < 1.5
 
 
@@ -110,6 +127,47 @@ def test_bench_two_ranks_rehearsal(gpu):
     assert line["results_allgather"]["bytes_per_rank"] == 2 * 65536
     assert line["c3"]["sizes"]["64"]["parity"]["mismatches"] == 0
     assert line["c4"]["parity"] == {"checked_packets": 2 * 200000, "mismatches": 0}
+    check_e2e(line["e2e"], 2)  # both ranks' host calls at once
+
+
+def test_bench_eight_ranks_rehearsal(gpu):
+    """the driver's 8-GPU command shape (`bench.py --gpus
+    8`, no torchrun environment: bench starts the 8 ranks itself) rehearsed
+    as 8 gloo ranks sharing cuda:0 at reduced sizes.  Every leg of the
+    default line runs on every rank: the headline shards, C5's strong split
+    (2^22 packets over 8 ranks: 2^19 each, one launch), the c3 / c4 / ring
+    legs, the e2e calls on all ranks at once, the results all-gather -- and
+    parity is checked on every rank.  The wall time is recorded for
+    DESIGN.md section 7."""
+    import time
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["WC_DIST_BACKEND"] = "gloo"
+    t0 = time.monotonic()
+    r = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "8",
+                        "--steps", "5", "--warmup", "1", "--packets", "65536",
+                        "--cpu-seconds", "0.3", *SMALL_C5, *SMALL_EXTRA],
+                       capture_output=True, text=True, timeout=600, cwd=ROOT, env=env)
+    wall = time.monotonic() - t0
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = _last_json(r.stdout)
+    print(f"8-rank rehearsal wall time {wall:.1f} s")
+    assert line["n_gpus"] == 8 and line["scaling"] == "weak"
+    assert line["config"]["parallelism"] == "packet-shard x8"
+    assert line["parity"] == {"checked_packets": 8 * 65536, "mismatches": 0}
+    g = line["results_allgather"]
+    assert g["ranks_mismatched"] == 0 and g["bytes_per_rank"] == 2 * 65536
+    c5 = line["c5"]
+    assert c5["n_gpus"] == 8 and "524288 packets per rank as 1 launch(es)" in c5["workload"]
+    assert c5["parity"]["checked_packets"] == 8 * (3 << 16) and c5["parity"]["mismatches"] == 0
+    for L, e in line["c3"]["sizes"].items():
+        K = -(-(64 << 20) // (65536 * int(L)))
+        assert e["parity"] == {"checked_packets": 8 * K * 65536, "mismatches": 0}, (L, e)
+    assert line["c4"]["parity"] == {"checked_packets": 8 * 200000, "mismatches": 0}
+    for name in ("rx_mtu", "zrx", "zrx_arp3"):
+        assert line["rings"][name]["parity"]["mismatches"] == 0, name
+    check_e2e(line["e2e"], 8)
+    assert 0 < line["roofline"]["frac_job"] < 1.5
 
 
 @pytest.mark.parametrize("args", [["--config", "c4", "--packets", "200000"],

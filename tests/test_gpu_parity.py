@@ -1133,6 +1133,118 @@ def test_host_server_light_traffic_then_full_batch(gpu, monkeypatch):
         wc.reload_config()
 
 
+def test_host_server_pause_bounds_device_sync(gpu):
+    """VERDICT r05 item 5.  Under steady small-batch traffic (one thread
+    issuing 1-packet registered calls back to back -- the RX drain of
+    backend_netmap.c:379-391) the resident grid never goes idle, so a
+    device-wide synchronisation in the same process waits as long as the
+    traffic lasts: 0.4 s of traffic here, a sync issued 0.1 s in.  After
+    wc_server_pause() the same sync returns at once while the traffic goes on
+    (on the zero-copy launch), every result is oracle-exact, the server
+    answers nothing while paused and answers again after wc_server_resume()."""
+    import threading
+    import time
+    rng = np.random.default_rng(55)
+    pool = rng.integers(0, 256, 64 * 2048, dtype=np.uint8)
+    one_off = np.array([3], dtype=np.uint64)
+    one_len = np.array([1472], dtype=np.uint16)
+    want1 = c_oracle.cksum_ragged(pool, one_off, one_len)
+    bad, calls = [], [0]
+    stop = threading.Event()
+
+    def traffic(seconds):
+        t_end = time.monotonic() + seconds
+        while not stop.is_set() and time.monotonic() < t_end:
+            got = wc.cksum_host(pool, one_off, one_len)
+            if got[0] != want1[0]:
+                bad.append(int(got[0]))
+            calls[0] += 1
+
+    wc.host_register(pool)
+    paused = False
+    try:
+        wc.cksum_host(pool, one_off, one_len)  # the grid up
+        # the hazard: a sync under steady traffic lasts as long as the traffic
+        th = threading.Thread(target=traffic, args=(0.4,))
+        th.start()
+        time.sleep(0.1)
+        t0 = time.monotonic()
+        torch.cuda.synchronize()
+        dt_unpaused = time.monotonic() - t0
+        th.join()
+        # the bound: pause, then sync, while the traffic goes on
+        th = threading.Thread(target=traffic, args=(30.0,))
+        th.start()
+        time.sleep(0.1)
+        s0 = wc.server_stats()
+        t0 = time.monotonic()
+        wc.server_pause()
+        paused = True
+        dt_pause = time.monotonic() - t0
+        t1 = time.monotonic()
+        torch.cuda.synchronize()
+        dt_sync = time.monotonic() - t1
+        s1 = wc.server_stats()
+        c1 = calls[0]
+        time.sleep(0.2)
+        s2 = wc.server_stats()
+        c2 = calls[0]
+        wc.server_resume()
+        paused = False
+        time.sleep(0.2)
+        stop.set()
+        th.join()
+        s3 = wc.server_stats()
+    finally:
+        stop.set()
+        if paused:
+            wc.server_resume()
+        wc.host_unregister(pool)
+    assert not bad, bad[:8]
+    assert dt_unpaused > 0.2, dt_unpaused  # waited for the traffic to end
+    assert dt_pause < 0.05 and dt_sync < 0.05, (dt_pause, dt_sync)
+    assert c2 - c1 > 100  # the traffic went on while paused ...
+    assert s2["served"] - s1["served"] <= 1, (s1, s2)  # ... on the zero-copy launch
+    assert s3["served"] - s2["served"] > 100, (s2, s3)  # and the server answers again
+    assert s3["fallbacks"] == s0["fallbacks"], (s0, s3)
+    with pytest.raises(wc.WcError):
+        wc.server_resume()  # (no pause to end)
+
+
+@pytest.mark.parametrize("register,serve", [(True, True), (True, False), (False, False)])
+def test_host_fused_ip_udp_short_len(gpu, monkeypatch, register, serve):
+    """an IPv4 header (with options) longer than `len`.  The
+    reference leaves payload_cksum(pkt, len < hl) undefined (its
+    `len - hl` wraps to ~4 GiB, in_cksum.c:164), but mk_ip4_hdr's header
+    checksum ip_cksum(pkt, hl) is defined whatever len is: the server, the
+    zero-copy launch and the pipeline all reload the header past len and
+    agree with the oracle on it."""
+    monkeypatch.setenv("WC_SERVE", "1" if serve else "0")
+    wc.reload_config()
+    rng = np.random.default_rng(7 + register + 2 * serve)
+    n, slot = 96, 256
+    pool = rng.integers(0, 256, n * slot + 64, dtype=np.uint8)
+    offs = (np.arange(n, dtype=np.uint64) * slot + rng.integers(0, 16, n).astype(np.uint64))
+    ihl = rng.integers(6, 16, n)
+    lens = np.array([int(rng.integers(20, 4 * h)) for h in ihl], dtype=np.uint16)  # 20 <= len < hl
+    for o, h in zip(offs.astype(np.int64), ihl):
+        pool[o] = 0x40 | h
+    want_h = c_oracle.cksum_ragged(pool, offs, (ihl * 4).astype(np.uint16), kind=0)
+    if register:
+        wc.host_register(pool)
+    s0 = wc.server_stats()
+    try:
+        got_h, _ = wc.cksum_ip_udp_host(pool, offs, lens)
+    finally:
+        if register:
+            wc.host_unregister(pool)
+        monkeypatch.delenv("WC_SERVE")
+        wc.reload_config()
+    s1 = wc.server_stats()
+    np.testing.assert_array_equal(got_h, want_h)
+    assert s1["served"] - s0["served"] == (1 if register and serve else 0)
+
+
 def test_host_register_after_free_and_reuse(gpu):
     """register -> free without unregister -> a new buffer mapped at the same
     address -> register again: the zero-copy path must read the NEW pages
@@ -1404,14 +1516,35 @@ def test_fused_tx_then_rx_roundtrip(gpu, monkeypatch, mode):
     assert (host(pay2)[p_nonzero] == 0).all()
 
 
+# Every path knob of the tuning build, each set to a value that would move
+# the C2 / C4 / RX paths if the shipped library read it.
+PATH_KNOBS = {"WC_DIAG_NOLOAD": "1", "WC_VARIANT": "64", "WC_SHAPE": "4,1,1",
+              "WC_BLOCKS_PER_CU": "1", "WC_GRID": "7", "WC_SEG": "0", "WC_SEG_ROWS": "8",
+              "WC_STRIDED_SEG": "2", "WC_LEAN_MAX": "0", "WC_LEAN_PHASE": "0", "WC_NT": "0",
+              "WC_GATHER": "0", "WC_GRP_DENSE": "0", "WC_SPLIT_PKTS": "1000",
+              "WC_SPLIT_BYTES": "4096", "WC_FLAT_UN": "1", "WC_FLAT_PK": "2",
+              "WC_RX_EARLY": "1", "WC_RX_HDRT": "0", "WC_RX_SKIP": "1", "WC_RX_ADAPT": "0",
+              "WC_RX_GRID": "3", "WC_ZC_BYTES": "0", "WC_RAGGED_SHAPE": "16,2,2"}
+
+
 def test_production_lib_ignores_tuning_knobs(gpu, monkeypatch):
-    """WC_DIAG_NOLOAD=1 (no-load timing kernel) and WC_VARIANT=64 (no result
-    store) are tuning-build knobs: the shipped library must ignore them and
-    stay oracle-exact on C2 and C4."""
-    assert "TUNING" not in wc.version()
-    monkeypatch.setenv("WC_DIAG_NOLOAD", "1")
-    monkeypatch.setenv("WC_VARIANT", "64")
-    wc.reload_config()
+    """The shipped library reads no path knob (VERDICT r02 item 2, r05 item
+    7): with every one of them set -- the result-dropping WC_VARIANT and the
+    no-load WC_DIAG_NOLOAD included -- and its configuration re-read, its
+    plan for C2 is the tuned table's and C2, C4 (both kinds) and an RX ring
+    stay oracle-exact.  (The calls go straight to the shipped library: it is
+    reloaded itself, not through wc.reload_config(), which would move them to
+    the tuning build.)"""
+    from warpcore_amd import _lib
+    lib = _lib.load()
+    assert "TUNING" not in wc.version() and not _lib.is_tuning(lib)
+    for k, v in PATH_KNOBS.items():
+        monkeypatch.setenv(k, v)
+    assert set(PATH_KNOBS) <= set(_lib.tuning_knobs())
+    lib.wc_config_reload()
+    assert _lib.active() is lib
+    p = wc.plan_strided(0x100000000, 1472, 1472, 1 << 20, kind="ip")
+    assert (p["group"], p["chunks_per_lane"], p["unroll"], p["kernel"]) == (32, 4, 1, "group")
     n, L = 1 << 20, 1472
     d = torch.empty(n * L + 64, dtype=torch.uint8, device=gpu)
     wc.synth_fill(d, synth.SEED, nbytes=n * L)
@@ -1429,6 +1562,14 @@ def test_production_lib_ignores_tuning_knobs(gpu, monkeypatch):
         np.testing.assert_array_equal(host(got), c_oracle.cksum_ragged(d[:total].cpu().numpy(),
                                                                        offs, lens, kind=k))
     del d
+    nf = 1 << 16
+    ring = torch.empty(nf * 2048 + 64, dtype=torch.uint8, device=gpu)
+    wc.synth_fill(ring, synth.SEED + 5, nbytes=nf * 2048)
+    f_off, f_len = synth.make_rx_ring(ring, nf, synth.zipf_lengths(nf, seed=9))
+    got, _ = wc.rx_verdict_ragged(ring, to_dev(f_off, gpu), to_dev(f_len, gpu))
+    np.testing.assert_array_equal(got.cpu().numpy(),
+                                  c_oracle.rx_verdict_ragged(ring.cpu().numpy(), f_off, f_len))
+    del ring
 
 
 LEAN_LENS = [16, 32, 48, 64, 80, 96, 128, 144, 192, 256, 320, 512, 576, 768]

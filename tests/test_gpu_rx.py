@@ -42,7 +42,12 @@ RX_MODES = {"default": {}, "ht": {"WC_RX_ADAPT": "0"},
             "skip": {"WC_RX_SKIP": "1"}, "skip_plain": {"WC_RX_SKIP": "1", "WC_RX_HDRT": "0"},
             "early": {"WC_RX_EARLY": "1"},
             "early_plain": {"WC_RX_EARLY": "1", "WC_RX_HDRT": "0"},
-            "early_skip": {"WC_RX_EARLY": "1", "WC_RX_SKIP": "1"}}
+            "early_skip": {"WC_RX_EARLY": "1", "WC_RX_SKIP": "1"},
+            # ADAPT's two tallying kernels pinned (the decision fixed, ADVICE
+            # r05), and a capped grid: each wave walks several tiles, the
+            # next tile's slots prefetched
+            "adapt_ht": {"WC_RX_FORCE": "1"}, "adapt_early": {"WC_RX_FORCE": "2"},
+            "grid4": {"WC_RX_GRID": "4"}, "grid4_early": {"WC_RX_GRID": "4", "WC_RX_EARLY": "1"}}
 
 
 @pytest.fixture(params=list(RX_MODES))

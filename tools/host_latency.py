@@ -9,6 +9,7 @@ backend's (backend_sock.c:145).
 """
 import argparse
 import os
+os.environ.setdefault("WC_TUNING", "1")  # the path knobs set below: the tuning build reads them
 import sys
 import time
 from pathlib import Path

@@ -16,6 +16,7 @@ from __future__ import annotations
 import argparse
 import ctypes
 import os
+os.environ.setdefault("WC_TUNING", "1")  # the path knobs set below: the tuning build reads them
 import statistics
 import subprocess
 import sys

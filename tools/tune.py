@@ -24,11 +24,10 @@ from pathlib import Path
 ROOT = Path(__file__).resolve().parent.parent
 sys.path.insert(0, str(ROOT))
 
-# WC_VARIANT / WC_DIAG_NOLOAD exist only in the tuning build (-DWC_TUNING,
-# libwccksum_tune.so): load it when a variant asks for them.
-if any(k in " ".join(sys.argv) for k in ("WC_VARIANT", "WC_DIAG_NOLOAD")) or \
-        any(k in os.environ for k in ("WC_VARIANT", "WC_DIAG_NOLOAD")):
-    os.environ.setdefault("WC_TUNING", "1")
+# The WC_* path knobs (and WC_VARIANT / WC_DIAG_NOLOAD) are read by the
+# tuning build alone (-DWC_TUNING, libwccksum_tune.so): every variant runs on
+# it, the default included.
+os.environ.setdefault("WC_TUNING", "1")
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -209,8 +208,11 @@ def main():
     if args.ceiling:
         slib = stream_lib()
         sink = torch.zeros(1 << 22, dtype=torch.int32, device=dev)
-        if args.config == "zslots":
-            # the ring's own lines, cheapest addressing (stream_ceiling.hip k_slot_read)
+        if args.config in ("zslots", "rx", "zrx"):
+            # the ring's own lines, cheapest addressing (stream_ceiling.hip
+            # k_slot_read): IP packets at +14 (zslots) or whole frames at +0
+            # of each 2048-B slot (rx / zrx: exactly the bytes the RX
+            # verdict's bandwidth is counted on)
             for grp in (4, 8, 16, 32):
                 for grid in (4096, 16384):
                     for nt in (0, 1):
@@ -268,7 +270,8 @@ def main():
                     fn = lambda: slib.tile_read(buf.data_ptr(), nbytes, g, u, nt,  # noqa: E731
                                                 sink.data_ptr(), stream.cuda_stream)
                 if name.startswith("SLOTREAD"):
-                    fn = lambda: slib.slot_read(buf.data_ptr(), 2048, 14,  # noqa: E731
+                    fn = lambda: slib.slot_read(buf.data_ptr(), 2048,  # noqa: E731
+                                                14 if args.config == "zslots" else 0,
                                                 d_len.data_ptr(), n, g, u, nt, sink.data_ptr(),
                                                 stream.cuda_stream)
                 fn()

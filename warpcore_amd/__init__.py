@@ -6,7 +6,8 @@ This package is the Python host mirror of that C ABI plus the synthetic
 packet generators and the multi-GPU shard driver used by bench.py.
 """
 from .cksum import (KIND_IP, KIND_PAYLOAD, SclkProbe, WcError, cksum_host, cksum_host_multi,
-                    cksum_ip_udp_host, server_stats,
+                    cksum_ip_udp_host, server_pause, server_paused, server_resume,
+                    server_stats,
                     cksum_ip_udp_ragged, cksum_ragged_multi, gather_results_multi,
                     gpu_init_multi, shard_range,
                     cksum_ip_udp_strided, cksum_ragged, cksum_strided, gpu_init, host_register, host_unregister,
@@ -18,7 +19,7 @@ from .cksum import (KIND_IP, KIND_PAYLOAD, SclkProbe, WcError, cksum_host, cksum
 
 __all__ = [
     "KIND_IP", "KIND_PAYLOAD", "SclkProbe", "WcError", "cksum_host", "cksum_host_multi",
-    "cksum_ip_udp_host", "server_stats",
+    "cksum_ip_udp_host", "server_pause", "server_paused", "server_resume", "server_stats",
     "cksum_ip_udp_ragged", "cksum_ragged_multi", "gather_results_multi", "gpu_init_multi",
     "shard_range",
     "cksum_ip_udp_strided", "cksum_ragged",

@@ -3,10 +3,12 @@
 * ``libwccksum.so`` -- the product: gfx950 HIP kernels + C ABI
   (``include/warpcore_gpu/wc_cksum.h``), built in-tree with ``hipcc`` so the
   ``.so`` travels with the repo snapshot to the GPU box.
-* ``libwccksum_tune.so`` -- the same sources with ``-DWC_TUNING``: the
-  experimental kernel branches (``WC_VARIANT``) and the timing-only no-load
-  kernel (``WC_DIAG_NOLOAD``) are live there and nowhere else.  Only
-  ``tools/`` loads it (``WC_TUNING=1``); it is never the default.
+* ``libwccksum_tune.so`` -- the same sources with ``-DWC_TUNING``: the only
+  build that reads the WC_* path knobs (kernel shapes, tile paths, RX modes),
+  and where the experimental kernel branches (``WC_VARIANT``) and the
+  timing-only no-load kernel (``WC_DIAG_NOLOAD``) are live.  ``tools/`` load
+  it (``WC_TUNING=1``), and the tests that pin each path against the oracle
+  reach it through ``warpcore_amd.reload_config()``; it is never the default.
 * ``oracle/libwc_oracle.so`` -- TEST INFRASTRUCTURE (parity checker / CPU
   baseline).  Built per host CPU model (``-march=native``), into
   ``oracle/build-<cpu>/`` so a box with a different host CPU rebuilds it.
@@ -37,8 +39,10 @@ HIP_SOURCES = [CSRC / "wc_k_strided.hip", CSRC / "wc_k_lean.hip", CSRC / "wc_k_s
                CSRC / "wc_k_flat.hip",
                CSRC / "wc_k_rx.hip", CSRC / "wc_k_serve.hip", CSRC / "wc_rccl.cpp",
                CSRC / "wc_k_synth.hip",
-               CSRC / "wc_cksum_api.cpp"]
+               CSRC / "wc_rt_config.cpp", CSRC / "wc_rt_plan.cpp", CSRC / "wc_rt_rx.cpp",
+               CSRC / "wc_rt_server.cpp", CSRC / "wc_rt_host.cpp", CSRC / "wc_rt_multi.cpp"]
 HIP_DEPS = HIP_SOURCES + [CSRC / "wc_cksum_kernels.h", CSRC / "wc_rccl.h", CSRC / "wc_device.h",
+                          CSRC / "wc_rt.h",
                           CSRC / "wc_flat.h", CSRC / "wc_seg.h",
                           INCLUDE / "warpcore_gpu" / "wc_cksum.h"]
 ORACLE_SOURCES = [ORACLE_DIR / "wc_oracle.c", ORACLE_DIR / "wc_oracle.h", ORACLE_DIR / "Makefile"]
@@ -147,7 +151,9 @@ def build_oracle(force: bool = False, verbose: bool = False) -> Path:
     return out
 
 
-def build_all(force: bool = False, verbose: bool = False, tuning: bool = False) -> None:
+def build_all(force: bool = False, verbose: bool = False, tuning: bool = True) -> None:
+    """The product library, the tuning build (the tests pin every path knob's
+    kernels through it) and the oracle."""
     build_lib(force=force, verbose=verbose)
     if tuning:
         build_lib(force=force, verbose=verbose, tuning=True)
@@ -155,4 +161,4 @@ def build_all(force: bool = False, verbose: bool = False, tuning: bool = False) 
 
 
 if __name__ == "__main__":
-    build_all(force="--force" in sys.argv, verbose=True, tuning="--tuning" in sys.argv)
+    build_all(force="--force" in sys.argv, verbose=True, tuning="--no-tuning" not in sys.argv)

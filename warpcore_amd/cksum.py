@@ -36,7 +36,7 @@ class WcError(RuntimeError):
     """A libwccksum call returned an error code."""
 
     def __init__(self, func: str, code: int):
-        msg = _lib.load().wc_strerror(code).decode()
+        msg = _lib.active().wc_strerror(code).decode()
         super().__init__(f"{func}: {msg} ({code})")
         self.code = code
 
@@ -70,8 +70,12 @@ def _dev_ptr(t: Union[torch.Tensor, int]) -> int:
 
 
 def reload_config() -> None:
-    """Re-read the WC_* tuning environment (read once at first init)."""
-    _check("wc_config_reload", _lib.load().wc_config_reload())
+    """Re-read the WC_* environment (read once at first init).  The shipped
+    library reads only the server's knobs (_lib.INTEGRATOR_KNOBS); while any
+    path knob (WC_SHAPE, WC_SEG, WC_RX_EARLY, ...) is set, the calls of this
+    module go to the tuning build, which reads them (tools and the tests that
+    pin every path against the oracle)."""
+    _check("wc_config_reload", _lib.select_for_env().wc_config_reload())
 
 
 def _span(length: int, kind: int) -> int:
@@ -187,7 +191,7 @@ def ip_cksum(buf, length: Optional[int] = None) -> int:
     p, n, keep = _host_buffer(buf, length)
     if keep.size < n:
         raise ValueError("buffer shorter than len")
-    return int(_lib.load().ip_cksum(p, n))
+    return int(_lib.active().ip_cksum(p, n))
 
 
 def payload_cksum(buf, length: Optional[int] = None) -> int:
@@ -195,7 +199,7 @@ def payload_cksum(buf, length: Optional[int] = None) -> int:
     p, n, keep = _host_buffer(buf, length)
     if keep.size < max(n, 20):
         raise ValueError("payload_cksum reads at least the 20-byte IPv4 header")
-    return int(_lib.load().payload_cksum(p, n))
+    return int(_lib.active().payload_cksum(p, n))
 
 
 # --------------------------------------------------------------------------
@@ -220,7 +224,7 @@ def cksum_strided(base: torch.Tensor, stride: int, length: int, n: int,
     _check_strided(base, byte_offset, stride, _check_len(length), n, k)
     out = _out_tensor(out, n, base.device)
     with _on_device(base.device):
-        _check("wc_cksum_strided", _lib.load().wc_cksum_strided(
+        _check("wc_cksum_strided", _lib.active().wc_cksum_strided(
             _dev_ptr(base) + byte_offset, stride, length, n, out.data_ptr(),
             k, _stream_ptr(stream, base.device)))
     return out
@@ -237,7 +241,7 @@ def cksum_ragged(base: torch.Tensor, offsets: torch.Tensor, lengths: torch.Tenso
     n = _check_ragged(base, offsets, lengths, k, check)
     out = _out_tensor(out, n, base.device)
     with _on_device(base.device):
-        _check("wc_cksum_ragged", _lib.load().wc_cksum_ragged(
+        _check("wc_cksum_ragged", _lib.active().wc_cksum_ragged(
             _dev_ptr(base), _dev_ptr(offsets), _dev_ptr(lengths), n, out.data_ptr(),
             k, _stream_ptr(stream, base.device)))
     return out
@@ -252,7 +256,7 @@ def verify_strided(base, stride, length, n, kind="payload", out=None,
     out = _out_tensor(out, n, base.device)
     bad = torch.zeros(1, dtype=torch.int64, device=base.device)
     with _on_device(base.device):
-        _check("wc_verify_strided", _lib.load().wc_verify_strided(
+        _check("wc_verify_strided", _lib.active().wc_verify_strided(
             _dev_ptr(base) + byte_offset, stride, length, n, out.data_ptr(), bad.data_ptr(),
             k, _stream_ptr(stream, base.device)))
     return out, bad
@@ -265,7 +269,7 @@ def verify_ragged(base, offsets, lengths, kind="payload", out=None,
     out = _out_tensor(out, n, base.device)
     bad = torch.zeros(1, dtype=torch.int64, device=base.device)
     with _on_device(base.device):
-        _check("wc_verify_ragged", _lib.load().wc_verify_ragged(
+        _check("wc_verify_ragged", _lib.active().wc_verify_ragged(
             _dev_ptr(base), _dev_ptr(offsets), _dev_ptr(lengths), n, out.data_ptr(),
             bad.data_ptr(), k, _stream_ptr(stream, base.device)))
     return out, bad
@@ -282,7 +286,7 @@ def cksum_ip_udp_strided(base: torch.Tensor, stride: int, length: int, n: int,
     hdr = _out_tensor(out_hdr, n, base.device)
     pay = _out_tensor(out, n, base.device)
     with _on_device(base.device):
-        _check("wc_cksum_ip_udp_strided", _lib.load().wc_cksum_ip_udp_strided(
+        _check("wc_cksum_ip_udp_strided", _lib.active().wc_cksum_ip_udp_strided(
             _dev_ptr(base) + byte_offset, stride, length, n, hdr.data_ptr(), pay.data_ptr(),
             _stream_ptr(stream, base.device)))
     return hdr, pay
@@ -295,7 +299,7 @@ def cksum_ip_udp_ragged(base: torch.Tensor, offsets: torch.Tensor, lengths: torc
     hdr = _out_tensor(out_hdr, n, base.device)
     pay = _out_tensor(out, n, base.device)
     with _on_device(base.device):
-        _check("wc_cksum_ip_udp_ragged", _lib.load().wc_cksum_ip_udp_ragged(
+        _check("wc_cksum_ip_udp_ragged", _lib.active().wc_cksum_ip_udp_ragged(
             _dev_ptr(base), _dev_ptr(offsets), _dev_ptr(lengths), n, hdr.data_ptr(),
             pay.data_ptr(), _stream_ptr(stream, base.device)))
     return hdr, pay
@@ -339,7 +343,7 @@ def rx_verdict_ragged(base: torch.Tensor, offsets: torch.Tensor, frame_lens: tor
           or not drops.is_contiguous() or drops.device != base.device):
         raise ValueError("drops must be a contiguous int64 / uint64 device tensor (accumulated)")
     with _on_device(base.device):
-        _check("wc_rx_verdict_ragged", _lib.load().wc_rx_verdict_ragged(
+        _check("wc_rx_verdict_ragged", _lib.active().wc_rx_verdict_ragged(
             _dev_ptr(base), _dev_ptr(offsets), _dev_ptr(frame_lens), n, out.data_ptr(),
             drops.data_ptr(), _stream_ptr(stream, base.device)))
     return out, drops
@@ -359,7 +363,7 @@ def rx_verdict_host(buf: np.ndarray, offsets: np.ndarray,
         raise ValueError("offsets and frame_lens must have the same shape")
     out = np.empty(off.size, dtype=np.uint8)
     drops = ctypes.c_uint64()
-    _check("wc_rx_verdict_host", _lib.load().wc_rx_verdict_host(
+    _check("wc_rx_verdict_host", _lib.active().wc_rx_verdict_host(
         buf.ctypes.data, buf.size, off.ctypes.data, lens.ctypes.data, off.size,
         out.ctypes.data, ctypes.byref(drops)))
     return out, int(drops.value)
@@ -386,7 +390,7 @@ def cksum_host(buf: np.ndarray, offsets: np.ndarray, lengths: np.ndarray,
     off = np.ascontiguousarray(offs_in, dtype=np.uint64)
     lens = np.ascontiguousarray(lens_in, dtype=np.uint16)
     out = np.empty(off.size, dtype=np.uint16)
-    _check("wc_cksum_host", _lib.load().wc_cksum_host(
+    _check("wc_cksum_host", _lib.active().wc_cksum_host(
         buf.ctypes.data, buf.size, off.ctypes.data, lens.ctypes.data, off.size,
         out.ctypes.data, _kind(kind)))
     return out
@@ -415,17 +419,40 @@ def cksum_ip_udp_host(buf: np.ndarray, offsets: np.ndarray,
     buf, off, lens = _host_batch_args(buf, offsets, lengths)
     hdr = np.empty(off.size, dtype=np.uint16)
     out = np.empty(off.size, dtype=np.uint16)
-    _check("wc_cksum_ip_udp_host", _lib.load().wc_cksum_ip_udp_host(
+    _check("wc_cksum_ip_udp_host", _lib.active().wc_cksum_ip_udp_host(
         buf.ctypes.data, buf.size, off.ctypes.data, lens.ctypes.data, off.size,
         hdr.ctypes.data, out.ctypes.data))
     return hdr, out
+
+
+def server_pause() -> None:
+    """Stop the resident server grid on every device (wc_server_pause); small
+    registered batches take the zero-copy launch until server_resume().  A
+    device-wide synchronisation then never waits for the grid."""
+    _check("wc_server_pause", _lib.active().wc_server_pause())
+
+
+def server_resume() -> None:
+    _check("wc_server_resume", _lib.active().wc_server_resume())
+
+
+class server_paused:
+    """``with server_paused(): ...`` -- server_pause() / server_resume()."""
+
+    def __enter__(self):
+        server_pause()
+        return self
+
+    def __exit__(self, *exc):
+        server_resume()
+        return False
 
 
 def server_stats() -> dict:
     """The resident server's counters (wc_server_stats): batches served,
     fallbacks to the launch path, grid launches -- process totals."""
     v = [ctypes.c_uint64() for _ in range(3)]
-    _check("wc_server_stats", _lib.load().wc_server_stats(*[ctypes.byref(x) for x in v]))
+    _check("wc_server_stats", _lib.active().wc_server_stats(*[ctypes.byref(x) for x in v]))
     return dict(zip(("served", "fallbacks", "launches"), (x.value for x in v)))
 
 
@@ -442,14 +469,14 @@ def host_register(buf: np.ndarray) -> None:
     same address) again re-pins the pages mapped there now."""
     if not isinstance(buf, np.ndarray) or not buf.flags["C_CONTIGUOUS"]:
         raise ValueError("host_register needs a C-contiguous numpy array")
-    _check("wc_host_register", _lib.load().wc_host_register(buf.ctypes.data, buf.nbytes))
+    _check("wc_host_register", _lib.active().wc_host_register(buf.ctypes.data, buf.nbytes))
     _registered[buf.ctypes.data] = buf
 
 
 def host_unregister(buf: np.ndarray) -> None:
     addr = buf.ctypes.data
     try:
-        _check("wc_host_unregister", _lib.load().wc_host_unregister(addr))
+        _check("wc_host_unregister", _lib.active().wc_host_unregister(addr))
     finally:
         _registered.pop(addr, None)
 
@@ -465,7 +492,7 @@ def synth_fill(buf: torch.Tensor, seed: int, nbytes: Optional[int] = None,
     if not 0 <= nbytes <= _nbytes(buf):
         raise ValueError(f"nbytes {nbytes} outside the {_nbytes(buf)}-byte buffer")
     with _on_device(buf.device):
-        _check("wc_synth_fill", _lib.load().wc_synth_fill(
+        _check("wc_synth_fill", _lib.active().wc_synth_fill(
             _dev_ptr(buf), nbytes, seed & 0xFFFFFFFFFFFFFFFF, _stream_ptr(stream, buf.device)))
     return buf
 
@@ -490,7 +517,7 @@ class SclkProbe:
         self.buf.zero_()
         self.stream.wait_stream(torch.cuda.current_stream(self.device))
         with _on_device(self.device):
-            _check("wc_sclk_probe", _lib.load().wc_sclk_probe(
+            _check("wc_sclk_probe", _lib.active().wc_sclk_probe(
                 self.buf.data_ptr(), self.n, every_us * 100, self.stream.cuda_stream))
 
     def mhz(self) -> float:
@@ -506,20 +533,20 @@ class SclkProbe:
 
 def plan_strided(base_addr: int, stride: int, length: int, n: int, kind="ip") -> dict:
     vals = [ctypes.c_int() for _ in range(4)]
-    _check("wc_plan_strided", _lib.load().wc_plan_strided(
+    _check("wc_plan_strided", _lib.active().wc_plan_strided(
         base_addr, stride, length, n, _kind(kind), *[ctypes.byref(v) for v in vals]))
     plan = dict(zip(("group", "chunks_per_lane", "unroll", "grid"), (v.value for v in vals)))
-    plan["kernel"] = _lib.load().wc_plan_strided_kernel(base_addr, stride, length, n,
+    plan["kernel"] = _lib.active().wc_plan_strided_kernel(base_addr, stride, length, n,
                                                         _kind(kind)).decode()
     return plan
 
 
 def gpu_init(device: int = -1) -> None:
-    _check("wc_gpu_init", _lib.load().wc_gpu_init(device))
+    _check("wc_gpu_init", _lib.active().wc_gpu_init(device))
 
 
 def version() -> str:
-    return _lib.load().wc_version().decode()
+    return _lib.active().wc_version().decode()
 
 
 # --------------------------------------------------------------------------
@@ -528,7 +555,7 @@ def version() -> str:
 def shard_range(n: int, g: int, ngpus: int) -> Tuple[int, int]:
     """The library's even contiguous split: packets [lo, hi) of n for shard g."""
     lo, hi = ctypes.c_uint64(), ctypes.c_uint64()
-    _check("wc_shard_range", _lib.load().wc_shard_range(n, g, ngpus, ctypes.byref(lo),
+    _check("wc_shard_range", _lib.active().wc_shard_range(n, g, ngpus, ctypes.byref(lo),
                                                         ctypes.byref(hi)))
     return lo.value, hi.value
 
@@ -544,15 +571,15 @@ def gpu_init_multi(ngpus: int = 0, devices=None) -> int:
         devices = [int(d) for d in devices]
         ngpus = len(devices)
         arr = (ctypes.c_int * ngpus)(*devices)
-    _check("wc_gpu_init_multi", _lib.load().wc_gpu_init_multi(ngpus, arr))
-    G = int(_lib.load().wc_gpu_multi_count())
+    _check("wc_gpu_init_multi", _lib.active().wc_gpu_init_multi(ngpus, arr))
+    G = int(_lib.active().wc_gpu_multi_count())
     _shard_devices = list(devices) if devices is not None else list(range(G))
     return G
 
 
 def shard_devices() -> list:
     """Device index of every shard executor (after gpu_init_multi)."""
-    G = int(_lib.load().wc_gpu_multi_count())
+    G = int(_lib.active().wc_gpu_multi_count())
     if len(_shard_devices) != G:
         raise RuntimeError("shard executors not set up by gpu_init_multi")
     return list(_shard_devices)
@@ -570,7 +597,7 @@ def cksum_host_multi(buf: np.ndarray, offsets: np.ndarray, lengths: np.ndarray,
     if off.shape != lens.shape:
         raise ValueError("offsets and lengths must have the same shape")
     out = np.empty(off.size, dtype=np.uint16)
-    _check("wc_cksum_host_multi", _lib.load().wc_cksum_host_multi(
+    _check("wc_cksum_host_multi", _lib.active().wc_cksum_host_multi(
         buf.ctypes.data, buf.size, off.ctypes.data, lens.ctypes.data, off.size,
         out.ctypes.data, _kind(kind)))
     return out
@@ -619,7 +646,7 @@ def cksum_ragged_multi(bases, offsets, lengths, outs, kind="ip", streams=None) -
         n = _check_ragged(b, o, l, k, True)
         _out_tensor(r, n, b.device)
     ns = (ctypes.c_uint64 * len(devs))(*[o.numel() for o in offsets])
-    _check("wc_cksum_ragged_multi", _lib.load().wc_cksum_ragged_multi(
+    _check("wc_cksum_ragged_multi", _lib.active().wc_cksum_ragged_multi(
         _ptrs(bases), _ptrs(offsets), _ptrs(lengths), ns, _ptrs(outs), k,
         _shard_streams(streams, devs)))
 
@@ -640,5 +667,5 @@ def gather_results_multi(shard_outs, counts, all_outs, streams=None) -> None:
         if a.numel() < total or a.element_size() != 2 or not a.is_contiguous():
             raise ValueError("each all_outs tensor needs sum(counts) contiguous 2-byte entries")
     ns = (ctypes.c_uint64 * len(devs))(*counts)
-    _check("wc_gather_results_multi", _lib.load().wc_gather_results_multi(
+    _check("wc_gather_results_multi", _lib.active().wc_gather_results_multi(
         _ptrs(shard_outs), ns, _ptrs(all_outs), _shard_streams(streams, devs)))

@@ -1,0 +1,318 @@
+// wc_rt_config.cpp -- configuration, per-device state and library lifetime
+// (wc_gpu_init / wc_gpu_fini / wc_config_reload / wc_strerror / wc_version).
+// There is no CPU checksum anywhere in this library: if no gfx950 device is
+// usable, batch calls return WC_ENODEV and the scalar drop-ins abort (the
+// reference's die(), util.h:280-340).
+
+#include "wc_rt.h"
+#include "wc_rccl.h"
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+namespace wc {
+namespace rt __attribute__((visibility("hidden"))) {
+
+FairMutex g_mu;
+Device g_dev[kMaxDevices];
+// Device d's state is built (set under g_mu once init_locked has finished it,
+// cleared by wc_gpu_fini): device-resident batch calls then only copy the
+// configuration (g_cfg_mu) and enqueue on the caller's stream, without
+// queueing behind a host-memory call that holds g_mu.
+std::atomic<bool> g_dev_ready[kMaxDevices];
+std::mutex g_cfg_mu; // g_cfg is written with g_mu AND g_cfg_mu held
+std::map<uintptr_t, Registration> g_registered; // host base -> region
+Config g_cfg;
+bool g_cfg_loaded = false;
+
+ShardExec g_shard[kMaxDevices];
+int g_multi_n = 0;
+
+int hip_err(hipError_t e) { return e == hipSuccess ? WC_OK : -(int)e; }
+
+int env_int(const char *name, int dflt)
+{
+    const char *v = getenv(name);
+    return (v && *v) ? atoi(v) : dflt;
+}
+
+uint64_t env_u64(const char *name, uint64_t dflt)
+{
+    const char *v = getenv(name);
+    return (v && *v) ? strtoull(v, nullptr, 0) : dflt;
+}
+
+bool parse_shape(const char *v, wc::Shape *sh)
+{
+    int g = 0, c = 0, u = 0;
+    if (!v || !*v || sscanf(v, "%d,%d,%d", &g, &c, &u) != 3)
+        return false;
+    *sh = {g, c, u};
+    return true;
+}
+
+void load_config_locked()
+{
+    // The shipped library's paths are the Config defaults above -- the table
+    // tuned on MI355X (DESIGN.md sections 4-5) -- and no environment changes
+    // them.  Only the resident server's sizing and lifetime are the
+    // integrator's: WC_SERVE, WC_SERVE_IDLE_US,
+    // WC_SERVE_WAVES, WC_SERVE_MAX (and WC_STAGE_THREADS, read by the staging
+    // pool).
+    Config c;
+    c.serve = env_int("WC_SERVE", c.serve);
+    c.serve_waves = std::max(1, std::min(env_int("WC_SERVE_WAVES", c.serve_waves), 1024));
+    c.serve_max = std::max(0, std::min(env_int("WC_SERVE_MAX", c.serve_max), (int)wc::kSrvMaxPkts));
+    c.serve_idle_us = std::max(100, env_int("WC_SERVE_IDLE_US", c.serve_idle_us));
+#ifdef WC_TUNING
+    // The tuning build (-DWC_TUNING, libwccksum_tune.so: tools/ and the
+    // tests that pin every path against the oracle) reads the path knobs.
+    // Each chooses among exact paths (shapes, grids, tile paths, load
+    // flavour) except WC_VARIANT (experimental kernel branches, one of which
+    // drops the result store) and WC_DIAG_NOLOAD (a timing-only kernel that
+    // reads no packet bytes).
+    c.blocks_per_cu = env_int("WC_BLOCKS_PER_CU", c.blocks_per_cu);
+    c.grid = env_int("WC_GRID", c.grid);
+    c.variant = env_int("WC_VARIANT", c.variant);
+    c.diag_noload = env_int("WC_DIAG_NOLOAD", c.diag_noload);
+    c.have_shape = parse_shape(getenv("WC_SHAPE"), &c.shape);
+    c.have_rshape = parse_shape(getenv("WC_RAGGED_SHAPE"), &c.rshape);
+    c.strided_seg = env_int("WC_STRIDED_SEG", c.strided_seg);
+    c.flat_un = env_int("WC_FLAT_UN", c.flat_un);
+    c.flat_tpw = env_int("WC_FLAT_TPW", c.flat_tpw);
+    c.seg = env_int("WC_SEG", c.seg);
+    c.seg_rows = env_int("WC_SEG_ROWS", c.seg_rows);
+    c.seg_rows_set = getenv("WC_SEG_ROWS") && *getenv("WC_SEG_ROWS");
+    c.zc_seg = env_int("WC_ZC_SEG", c.zc_seg);
+    c.zc_group_max = env_int("WC_ZC_GROUP_MAX", c.zc_group_max);
+    c.zc_bytes = env_int("WC_ZC_BYTES", c.zc_bytes);
+    c.flat_min = env_u64("WC_FLAT_MIN", c.flat_min);
+    c.nt = env_int("WC_NT", c.nt);
+    c.grp_dense = env_int("WC_GRP_DENSE", c.grp_dense);
+    c.grp_sparse = env_int("WC_GRP_SPARSE", c.grp_sparse);
+    c.grp_rows = env_int("WC_GRP_ROWS", c.grp_rows);
+    c.flat_pk = env_int("WC_FLAT_PK", c.flat_pk);
+    c.gather = env_int("WC_GATHER", c.gather);
+    c.lean_max = env_int("WC_LEAN_MAX", c.lean_max);
+    c.split_bytes = env_u64("WC_SPLIT_BYTES", c.split_bytes);
+    c.split_pkts = env_u64("WC_SPLIT_PKTS", c.split_pkts);
+    c.lean_phase = env_int("WC_LEAN_PHASE", c.lean_phase);
+    c.serve_prio = env_int("WC_SERVE_PRIO", c.serve_prio) != 0;
+    c.rx_early = env_int("WC_RX_EARLY", c.rx_early);
+    c.rx_hdrt = env_int("WC_RX_HDRT", c.rx_hdrt);
+    c.rx_skip = env_int("WC_RX_SKIP", c.rx_skip);
+    c.rx_adapt = env_int("WC_RX_ADAPT", c.rx_adapt);
+    c.rx_trace = env_int("WC_RX_TRACE", c.rx_trace);
+    c.rx_force = env_int("WC_RX_FORCE", c.rx_force);
+    c.rx_grid = std::max(0, env_int("WC_RX_GRID", c.rx_grid));
+#endif
+    {
+        std::lock_guard<std::mutex> lk(g_cfg_mu);
+        g_cfg = c;
+    }
+    g_cfg_loaded = true;
+}
+
+int current_device(int *dev)
+{
+    int d = 0;
+    hipError_t e = hipGetDevice(&d);
+    if (e != hipSuccess)
+        return hip_err(e);
+    if (d < 0 || d >= kMaxDevices)
+        return WC_ENODEV;
+    *dev = d;
+    return WC_OK;
+}
+
+// Create per-device state (caller holds g_mu).
+int init_locked(int device, Device **out)
+{
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return WC_ENODEV;
+    if (device >= 0) {
+        if (device >= ndev || device >= kMaxDevices)
+            return WC_EINVAL;
+        hipError_t e = hipSetDevice(device);
+        if (e != hipSuccess)
+            return hip_err(e);
+    } else {
+        int rc = current_device(&device);
+        if (rc)
+            return rc;
+    }
+    if (!g_cfg_loaded)
+        load_config_locked();
+    Device &D = g_dev[device];
+    if (!D.ok) {
+        hipDeviceProp_t prop;
+        hipError_t e = hipGetDeviceProperties(&prop, device);
+        if (e != hipSuccess)
+            return hip_err(e);
+        if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+            fprintf(stderr, "wccksum: device %d is %s, this build targets gfx950\n",
+                    device, prop.gcnArchName);
+            return WC_ENODEV;
+        }
+        D.cus = prop.multiProcessorCount;
+        int khz = 0;
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess &&
+            khz > 0)
+            D.clock_khz = (uint64_t)khz;
+        e = hipStreamCreateWithFlags(&D.scalar_st, hipStreamNonBlocking);
+        if (e != hipSuccess)
+            return hip_err(e);
+        e = hipHostMalloc((void **)&D.h_stage, kScalarStage,
+                          hipHostMallocMapped | hipHostMallocCoherent);
+        if (e != hipSuccess)
+            return WC_ENOMEM;
+        e = hipHostMalloc((void **)&D.h_res, 64,
+                          hipHostMallocMapped | hipHostMallocCoherent);
+        if (e != hipSuccess)
+            return WC_ENOMEM;
+        if (hipHostGetDevicePointer((void **)&D.d_stage, D.h_stage, 0) != hipSuccess ||
+            hipHostGetDevicePointer((void **)&D.d_res, D.h_res, 0) != hipSuccess)
+            return WC_ENOMEM;
+        for (int k = 0; k < kRxSets; ++k) {
+            if (hipHostMalloc((void **)&D.h_rx_tally[k], wc::kRxTallyWords * 4,
+                              hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+                hipHostGetDevicePointer((void **)&D.d_rx_tally[k], D.h_rx_tally[k], 0) !=
+                    hipSuccess)
+                return WC_ENOMEM;
+            memset(D.h_rx_tally[k], 0, wc::kRxTallyWords * 4);
+        }
+        D.ok = true;
+        g_dev_ready[device].store(true, std::memory_order_release);
+    }
+    *out = &D;
+    return WC_OK;
+}
+
+// The device-resident batch calls' entry: the current device's state and a
+// copy of the configuration.  Once the device is set up this takes only the
+// configuration lock (held for the copy), never g_mu.
+int ensure_device(Device **out, Config *cfg)
+{
+    int dev = 0;
+    if (current_device(&dev) == WC_OK && g_dev_ready[dev].load(std::memory_order_acquire)) {
+        *out = &g_dev[dev];
+        std::lock_guard<std::mutex> lk(g_cfg_mu);
+        *cfg = g_cfg;
+        return WC_OK;
+    }
+    std::lock_guard<FairMutex> lk(g_mu);
+    const int rc = init_locked(-1, out);
+    if (rc == WC_OK) {
+        std::lock_guard<std::mutex> lc(g_cfg_mu);
+        *cfg = g_cfg;
+    }
+    return rc;
+}
+
+} // namespace rt
+} // namespace wc
+
+using namespace wc::rt;
+
+extern "C" {
+
+int wc_gpu_init(int device)
+{
+    std::lock_guard<FairMutex> lk(g_mu);
+    Device *D = nullptr;
+    return init_locked(device, &D);
+}
+
+int wc_gpu_fini(void)
+{
+    std::lock_guard<FairMutex> lk(g_mu);
+    int cur = 0;
+    const bool have_cur = hipGetDevice(&cur) == hipSuccess;
+    for (int d = 0; d < kMaxDevices; ++d) // (device calls take the locked path again)
+        g_dev_ready[d].store(false, std::memory_order_release);
+    server_stop_all_locked();
+    wc::rccl_fini();
+    for (int g = 0; g < g_multi_n; ++g) {
+        (void)hipSetDevice(g_shard[g].dev);
+        pipe_free(g_shard[g].pipe);
+        g_shard[g] = ShardExec{};
+    }
+    g_multi_n = 0;
+    for (int d = 0; d < kMaxDevices; ++d) {
+        Device &D = g_dev[d];
+        if (!D.ok)
+            continue;
+        (void)hipSetDevice(d);
+        pipe_free(D.pipe);
+        if (D.zc.ready) {
+            (void)hipStreamSynchronize(D.zc.st);
+            (void)hipStreamDestroy(D.zc.st);
+            (void)hipHostFree(D.zc.h_off);
+            (void)hipHostFree(D.zc.h_len);
+            (void)hipHostFree(D.zc.h_out);
+            (void)hipHostFree(D.zc.h_out2);
+        }
+        if (D.srv.ready) {
+            (void)hipStreamDestroy(D.srv.st);
+            (void)hipHostFree(D.srv.h_rec);
+            (void)hipHostFree(D.srv.h_res);
+            (void)hipHostFree(D.srv.h_hb);
+        }
+        (void)hipStreamSynchronize(D.scalar_st);
+        (void)hipDeviceSynchronize(); // (an RX launch may still write its tally)
+        // Under g_rx_mu: rx_launch reads and clears the tallies holding only
+        // that lock (device calls skip g_mu), so it never sees them freed.
+        std::lock_guard<std::mutex> lr(g_rx_mu);
+        for (int k = 0; k < kRxSets; ++k)
+            (void)hipHostFree(D.h_rx_tally[k]);
+        (void)hipStreamDestroy(D.scalar_st);
+        (void)hipHostFree(D.h_stage);
+        (void)hipHostFree(D.h_res);
+        D = Device{};
+    }
+    // Page-locks taken with wc_host_register belong to the caller and stay
+    // until wc_host_unregister (a ring registered once keeps its zero-copy
+    // path across fini / init).  The WC_* configuration is re-read at the
+    // next initialisation.
+    g_cfg_loaded = false;
+    if (have_cur)
+        (void)hipSetDevice(cur);
+    return WC_OK;
+}
+
+int wc_config_reload(void)
+{
+    std::lock_guard<FairMutex> lk(g_mu);
+    load_config_locked();
+    return WC_OK;
+}
+
+const char *wc_strerror(int err)
+{
+    switch (err) {
+    case WC_OK:
+        return "success";
+    case WC_EINVAL:
+        return "invalid argument";
+    case WC_ENODEV:
+        return "no usable gfx950 device";
+    case WC_ENOMEM:
+        return "out of memory";
+    case WC_ECOMM:
+        return "RCCL unavailable or collective failed";
+    default:
+        if (err < 0 && err > -10000)
+            return hipGetErrorString((hipError_t)(-err));
+        return "unknown error";
+    }
+}
+
+#ifdef WC_TUNING
+const char *wc_version(void) { return "wccksum 0.3.0 (gfx950, TUNING build: WC_VARIANT/WC_DIAG_NOLOAD live)"; }
+#else
+const char *wc_version(void) { return "wccksum 0.3.0 (gfx950)"; }
+#endif
+
+} // extern "C"
