@@ -790,12 +790,21 @@ def e2e_leg(args, dev, rank, world, coll_dev):
     pinned.copy_(torch.from_numpy(c2))
     pageable = torch.from_numpy(c2)
     ceiling = {}
-    for name, src in (("pinned", pinned), ("pageable", pageable)):
+    for name, src in (("pinned", pinned), ("registered", pageable), ("pageable", pageable)):
+        # pinned: torch's page-locked allocation (hipHostMalloc); registered:
+        # the same numpy bytes page-locked in place (wc_host_register, as a
+        # netmap region would be); pageable: plain memory
         def copy(src=src):
             d[: n * L].copy_(src, non_blocking=True)
             torch.cuda.synchronize(dev)
-        copy()
-        best, _ = timed(copy)
+        if name == "registered":
+            wc.host_register(c2)
+        try:
+            copy()
+            best, _ = timed(copy)
+        finally:
+            if name == "registered":
+                wc.host_unregister(c2)
         ceiling[name] = round(world * n * L / best / 1e9, 2)
     del pinned, pageable, d
     torch.cuda.empty_cache()
@@ -840,6 +849,7 @@ def e2e_leg(args, dev, rank, world, coll_dev):
                 "GBps": round(gbps, 2), "GBps_median": round(world * nbytes / med / 1e9, 2),
                 "ms_best": round(best * 1e3, 3),
                 "frac_of_h2d_pinned": round(gbps / ceiling["pinned"], 4),
+                "frac_of_h2d_same_memory": round(gbps / ceiling[kind], 4),
                 "parity": {"checked_packets": wdist.sum_over_ranks(2 * n, coll_dev),
                            "mismatches": wdist.sum_over_ranks(bad, coll_dev)}}
     rx_ok = int(np.isin(want_rx, (0, 1)).sum())
@@ -853,7 +863,9 @@ def e2e_leg(args, dev, rank, world, coll_dev):
                      f"its own link; best of {reps}"),
         "n_ranks": world,
         "h2d_ceiling_GBps": {**ceiling, "how": "torch copy_ of the C2 bytes to the device "
-                                              "(hipMemcpyAsync H2D), best of %d" % reps},
+                                              "(hipMemcpyAsync H2D) from a hipHostMalloc'd "
+                                              "buffer, from the region page-locked in place, "
+                                              "and from pageable memory; best of %d" % reps},
         "calls": res,
         "rx_frames_ok": wdist.sum_over_ranks(rx_ok, coll_dev),
     }

@@ -14,6 +14,9 @@
 #   prof_c2       rocprofv3 --kernel-trace --stats of the driver's headline command
 #   diag_headline tools/diag_headline.py (the headline's whole-job gap, by issue mode)
 #   tune          tools/tune.py $TUNE_ARGS (> tune.log)
+#   e2e           tools/e2e.py $E2E_ARGS (host-path variants, end to end)
+#   ab            A/B of WC_LIB=$AB_LIB against the in-tree library, tune.py $AB_ARGS
+#                 (';'-separated cases), $AB_REPS alternating rounds
 #   round         tools/round_measure.sh with CFGS (bench line + rocprof + PMC passes)
 #   pmc           one rocprofv3 --pmc pass per counter group in PMC_GROUPS ("A B;C D")
 #                 over bench.py $PMC_BENCH_ARGS
@@ -41,7 +44,7 @@ step() {  # $1 = name, $2 = seconds, rest = command; stdout/stderr -> $OUT/$1.lo
 for s in ${STEPS:-pytest smoke bench}; do
     case $s in
         pytest)
-            step pytest 1400 python -u -m pytest tests -m gpu -x -q --timeout 300 \
+            step pytest 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 \
                 --timeout-method thread ${PYTEST_ARGS:-} ;;
         smoke)
             step smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
@@ -61,6 +64,21 @@ for s in ${STEPS:-pytest smoke bench}; do
             step diag_headline 300 python tools/diag_headline.py --json "$OUT/diag_headline.json" ;;
         tune)
             step tune 600 python tools/tune.py ${TUNE_ARGS:-} ;;
+        e2e)
+            step e2e 500 python tools/e2e.py ${E2E_ARGS:-} ;;
+        ab)
+            # A/B of two builds in alternating fresh processes: WC_LIB=$AB_LIB
+            # (A) against the in-tree product library (B), tune.py $AB_ARGS
+            # for each ';'-separated case, $AB_REPS times.
+            IFS=';' read -ra cases <<< "${AB_ARGS:---config zrx}"
+            for rep in $(seq 1 "${AB_REPS:-3}"); do
+                c=0
+                for a in "${cases[@]}"; do
+                    c=$((c + 1))
+                    step ab_A${c}_$rep 200 env WC_TUNING=0 WC_LIB="$AB_LIB" python tools/tune.py $a --rounds 3 --iters 20
+                    step ab_B${c}_$rep 200 env WC_TUNING=0 WC_LIB="$REPO/warpcore_amd/libwccksum.so" python tools/tune.py $a --rounds 3 --iters 20
+                done
+            done ;;
         round)
             step round 1200 env TAG="$TAG" CFGS="${CFGS:-c2}" bash tools/round_measure.sh ;;
         pmc)

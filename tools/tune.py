@@ -50,7 +50,22 @@ def stream_lib():
     lib.slot_read.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p,
                               ctypes.c_uint64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                               ctypes.c_void_p, ctypes.c_void_p]
+    lib.line_read.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int,
+                              ctypes.c_void_p, ctypes.c_void_p]
     return lib
+
+
+def touched_lines(offs: np.ndarray, lens: np.ndarray, line: int = 128) -> np.ndarray:
+    """uint32 indices of every `line`-byte line the ranges [off, off + len)
+    touch, in range order (each line once per range)."""
+    offs = offs.astype(np.int64)
+    lens = lens.astype(np.int64)
+    keep = lens > 0
+    first = offs[keep] // line
+    last = (offs[keep] + lens[keep] - 1) // line
+    cnt = last - first + 1
+    start = np.repeat(np.cumsum(cnt) - cnt, cnt)
+    return (np.repeat(first, cnt) + (np.arange(int(cnt.sum())) - start)).astype(np.uint32)
 
 
 def time_it(fn, iters, stream):
@@ -213,10 +228,17 @@ def main():
             # k_slot_read): IP packets at +14 (zslots) or whole frames at +0
             # of each 2048-B slot (rx / zrx: exactly the bytes the RX
             # verdict's bandwidth is counted on)
-            for grp in (4, 8, 16, 32):
-                for grid in (4096, 16384):
-                    for nt in (0, 1):
+            for grp in (8, 16):
+                for grid in (16384,):
+                    for nt in (1,):
                         cases.append((f"SLOTREAD G={grp} grid={grid} nt={nt}", (grp, grid, nt)))
+            # exactly the 128-B lines the ring's packets / frames touch, read once
+            r_off, r_len = (offs, lens) if args.config == "zslots" else (f_off, f_len)
+            d_lines = torch.from_numpy(touched_lines(r_off, r_len)).to(dev)
+            print(f"LINEREAD: {d_lines.numel()} lines = {d_lines.numel() * 128 / nbytes:.3f} x "
+                  f"the counted bytes", flush=True)
+            for u in (1, 2, 4, 8):
+                cases.append((f"LINEREAD U={u}", (u, 0, 0)))
         else:
             for region in (4096, 8192, 16384, 32768, 65536):
                 for mode in (0, 1):
@@ -269,6 +291,10 @@ def main():
                 if name.startswith("TILEREAD"):
                     fn = lambda: slib.tile_read(buf.data_ptr(), nbytes, g, u, nt,  # noqa: E731
                                                 sink.data_ptr(), stream.cuda_stream)
+                if name.startswith("LINEREAD"):
+                    fn = lambda: slib.line_read(buf.data_ptr(), d_lines.data_ptr(),  # noqa: E731
+                                                d_lines.numel(), g, sink.data_ptr(),
+                                                stream.cuda_stream)
                 if name.startswith("SLOTREAD"):
                     fn = lambda: slib.slot_read(buf.data_ptr(), 2048,  # noqa: E731
                                                 14 if args.config == "zslots" else 0,

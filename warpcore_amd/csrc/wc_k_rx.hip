@@ -195,16 +195,28 @@ __device__ __forceinline__ void rx_load_t(uint64_t fa, uint32_t flen, bool valid
     c4 = load_chunk<false>(lv != 0u && (fa & 15u) > 2u && a4 < fa + lv ? a4 : zero);
 }
 
+// The hand-off is XOR-swizzled: chunk j of frame f sits in slot
+// 4 f + (j ^ ((f >> 2) & 3)).  Unswizzled (slot 4 f + j), the read of chunk k
+// by lane f -- 16 B at a 64-B lane stride -- put the four lanes f, f + 4,
+// f + 8, f + 12 of a ds_read_b128 lane group on the same banks (bank =
+// (address / 4) mod 64): a 4-way conflict on every read, 2.85 M conflict
+// cycles on the mixed-size ring against 1.28 M for the plain stream
+// (profiles/pmc_r05_rx_instr.txt).  Swizzled, each 16-lane group reads 16
+// distinct 16-B bank slots (its lanes are 16 distinct residues mod 16), and
+// the stores stay conflict-free (each 8-lane ds_write_b128 group still
+// covers 8 consecutive slots, permuted).
 __device__ __forceinline__ void rx_hdr_gather(u32x4 *stage, int lane, const u32x4 (&hx)[4],
                                               const u32x4 &c4, u32x4 (&c)[5])
 {
+    const int ws = lane ^ ((lane >> 4) & 3); // frame 16 i + lane / 4, chunk lane % 4
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-        stage[64 * i + lane] = hx[i]; // frame 16 i + lane / 4, chunk lane % 4
+        stage[64 * i + ws] = hx[i];
     wave_order();
+    const int rs = (lane >> 2) & 3;
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-        c[k] = stage[4 * lane + k];
+        c[k] = stage[4 * lane + (k ^ rs)];
     c[4] = c4;
     wave_order(); // stage is rewritten by the stream's first row group
 }

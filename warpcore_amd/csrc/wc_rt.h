@@ -75,6 +75,22 @@ struct ZeroCopy {
     bool ready = false;
 };
 
+// Large batches in a registered region, read by the kernels in place over
+// PCIe (host_zc_stream): chunks of up to kZsPkts packets, one launch each,
+// their offsets / lengths / results double-buffered in mapped pinned memory.
+// Only the lines the packets touch cross the link -- not the gaps between
+// netmap slots the pipeline's range copy ships -- and nothing is staged.
+constexpr uint64_t kZsPkts = 1ull << 16;
+struct ZcStream {
+    hipStream_t st = nullptr;
+    hipEvent_t done[2] = {};
+    uint64_t *h_off[2] = {}, *d_off[2] = {}; // mapped pinned
+    uint16_t *h_len[2] = {}, *d_len[2] = {};
+    uint16_t *h_out[2] = {}, *d_out[2] = {};
+    uint16_t *h_out2[2] = {}, *d_out2[2] = {}; // fused pass: header checksums
+    bool ready = false;
+};
+
 // The resident small-batch server of one device (wc_k_serve.hip): its
 // stream, the mapped pinned request records and result slots, the request
 // counter, and whether its grid is running.
@@ -110,6 +126,7 @@ struct Device {
     uint16_t *d_res = nullptr;
     HostPipe pipe;
     ZeroCopy zc;
+    ZcStream zs;
     Server srv;
     // RX verdict ADAPT mode: kRxSets tally arrays in mapped pinned memory,
     // one per recent launch (launch g writes set g % kRxSets), and the mode
@@ -152,6 +169,7 @@ struct Config {
     int zc_seg = 0;                // WC_ZC_SEG: seg kernel on zero-copy batches
     int zc_group_max = (int)kZcGroupMax; // WC_ZC_GROUP_MAX
     int zc_bytes = kZcBytesDefault;      // WC_ZC_BYTES
+    int zc_stream = 1;             // WC_ZC_STREAM: large registered batches read in place (0: pipeline)
     uint64_t flat_min = kFlatMinDefault; // WC_FLAT_MIN: ragged group kernel below this n
     int diag_noload = 0;           // WC_DIAG_NOLOAD: timing-only kernel (tuning build)
     int nt = 1;                    // WC_NT: nontemporal loads
@@ -303,6 +321,7 @@ bool server_enabled_locked();
 
 // --- wc_rt_host.cpp -----------------------------------------------------------
 void pipe_free(HostPipe &P);
+void zs_free(ZcStream &S);
 int pipe_init_locked(HostPipe &P);
 const uint8_t *registered_dptr_locked(const void *p, uint64_t bytes);
 uint64_t span_of(uint16_t len, int kind);

@@ -87,6 +87,7 @@ void load_config_locked()
     c.zc_seg = env_int("WC_ZC_SEG", c.zc_seg);
     c.zc_group_max = env_int("WC_ZC_GROUP_MAX", c.zc_group_max);
     c.zc_bytes = env_int("WC_ZC_BYTES", c.zc_bytes);
+    c.zc_stream = env_int("WC_ZC_STREAM", c.zc_stream);
     c.flat_min = env_u64("WC_FLAT_MIN", c.flat_min);
     c.nt = env_int("WC_NT", c.nt);
     c.grp_dense = env_int("WC_GRP_DENSE", c.grp_dense);
@@ -254,6 +255,7 @@ int wc_gpu_fini(void)
             (void)hipHostFree(D.zc.h_out);
             (void)hipHostFree(D.zc.h_out2);
         }
+        zs_free(D.zs);
         if (D.srv.ready) {
             (void)hipStreamDestroy(D.srv.st);
             (void)hipHostFree(D.srv.h_rec);

@@ -182,6 +182,101 @@ int host_zero_copy(Device &D, const uint8_t *dbase, const uint64_t *h_off,
     return WC_OK;
 }
 
+int zs_init_locked(Device &D)
+{
+    ZcStream &S = D.zs;
+    if (S.ready)
+        return WC_OK;
+    const unsigned fl = hipHostMallocMapped | hipHostMallocCoherent;
+    bool ok = hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking) == hipSuccess;
+    for (int b = 0; b < 2 && ok; ++b)
+        ok = hipEventCreateWithFlags(&S.done[b], hipEventDisableTiming) == hipSuccess &&
+             hipHostMalloc((void **)&S.h_off[b], kZsPkts * 8, fl) == hipSuccess &&
+             hipHostMalloc((void **)&S.h_len[b], kZsPkts * 2, fl) == hipSuccess &&
+             hipHostMalloc((void **)&S.h_out[b], kZsPkts * 2, fl) == hipSuccess &&
+             hipHostMalloc((void **)&S.h_out2[b], kZsPkts * 2, fl) == hipSuccess &&
+             hipHostGetDevicePointer((void **)&S.d_off[b], S.h_off[b], 0) == hipSuccess &&
+             hipHostGetDevicePointer((void **)&S.d_len[b], S.h_len[b], 0) == hipSuccess &&
+             hipHostGetDevicePointer((void **)&S.d_out[b], S.h_out[b], 0) == hipSuccess &&
+             hipHostGetDevicePointer((void **)&S.d_out2[b], S.h_out2[b], 0) == hipSuccess;
+    if (!ok) {
+        zs_free(S);
+        return WC_ENOMEM;
+    }
+    S.ready = true;
+    return WC_OK;
+}
+
+void zs_free(ZcStream &S)
+{
+    if (S.st)
+        (void)hipStreamSynchronize(S.st);
+    for (int b = 0; b < 2; ++b) {
+        if (S.done[b])
+            (void)hipEventDestroy(S.done[b]);
+        (void)hipHostFree(S.h_off[b]);
+        (void)hipHostFree(S.h_len[b]);
+        (void)hipHostFree(S.h_out[b]);
+        (void)hipHostFree(S.h_out2[b]);
+    }
+    if (S.st)
+        (void)hipStreamDestroy(S.st);
+    S = ZcStream{};
+}
+
+// A large batch in a registered region (ZcStream): chunk k's launch reads
+// its packets in place while the host writes chunk k + 1's offsets and
+// lengths into the other buffer and copies chunk k - 1's results out.
+int host_zc_stream(Device &D, const uint8_t *dbase, const uint64_t *h_off,
+                   const uint16_t *h_len, uint64_t n, uint8_t *h_out, int kind,
+                   uint16_t *h_out2)
+{
+    int rc = zs_init_locked(D);
+    if (rc)
+        return rc;
+    ZcStream &S = D.zs;
+    const int osz = out_size(kind);
+    uint64_t pend_lo[2] = {}, pend_n[2] = {};
+    bool pend[2] = {};
+    auto drain = [&](int b) -> int {
+        if (!pend[b])
+            return WC_OK;
+        const hipError_t e = hipEventSynchronize(S.done[b]);
+        if (e != hipSuccess)
+            return hip_err(e);
+        memcpy(h_out + pend_lo[b] * osz, (const void *)S.h_out[b], pend_n[b] * osz);
+        if (kind == kKindFused)
+            memcpy(h_out2 + pend_lo[b], (const void *)S.h_out2[b], pend_n[b] * 2);
+        pend[b] = false;
+        return WC_OK;
+    };
+    int b = 0;
+    for (uint64_t i = 0; i < n && rc == WC_OK; i += kZsPkts, b ^= 1) {
+        const uint64_t cnt = std::min(kZsPkts, n - i);
+        rc = drain(b); // (chunk k - 2's results: its buffers are free again)
+        if (rc)
+            break;
+        memcpy(S.h_off[b], h_off + i, cnt * 8);
+        memcpy(S.h_len[b], h_len + i, cnt * 2);
+        rc = run_ragged_any(D, g_cfg, dbase, S.d_off[b], S.d_len[b], cnt, S.d_out[b], kind, true,
+                            S.st, S.d_out2[b]);
+        if (rc == WC_OK)
+            rc = hip_err(hipEventRecord(S.done[b], S.st));
+        if (rc == WC_OK) {
+            pend[b] = true;
+            pend_lo[b] = i;
+            pend_n[b] = cnt;
+        }
+    }
+    if (rc == WC_OK)
+        rc = drain(b); // the older of the two in flight first
+    if (rc == WC_OK)
+        rc = drain(b ^ 1);
+    if (rc != WC_OK) // (nothing may still write the mapped buffers the next call refills)
+        (void)hipStreamSynchronize(S.st);
+    return rc;
+}
+
 // Library-owned staging workers.  Pageable input reaches the GPU through
 // the pinned staging ring, and copying it there was the end-to-end path's
 // limit on one thread (24.6-28.9 GB/s against ~55 GB/s for DMA from
@@ -527,6 +622,8 @@ int host_batch(const void *h_base, uint64_t h_bytes, const uint64_t *h_off,
     }
     if (dbase && n <= kZcPkts && total <= (uint64_t)g_cfg.zc_bytes)
         return host_zero_copy(*D, dbase, h_off, h_len, n, h_out, kind, h_out2);
+    if (dbase && g_cfg.zc_stream)
+        return host_zc_stream(*D, dbase, h_off, h_len, n, h_out, kind, h_out2);
     rc = pipe_init_locked(D->pipe);
     if (rc)
         return rc;
