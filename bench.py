@@ -682,8 +682,10 @@ def c5_leg(args, dev, rank, world, coll_dev):
     for _ in range(steps):
         step()
     ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0  # (as the headline: to this rank's synchronize)
     wdist.barrier(dev)
-    elapsed = wdist.max_over_ranks(time.perf_counter() - t0, coll_dev)
+    elapsed = wdist.max_over_ranks(elapsed, coll_dev)
     kernel_ms = wdist.max_over_ranks(ev0.elapsed_time(ev1) / steps / launches, coll_dev)
     total_bytes = float(args.total_packets) * L * steps
     gbps = total_bytes / elapsed / 1e9
@@ -1014,9 +1016,12 @@ def main():
     # captured once: one replay, no Python launch cost between t0 and the
     # first kernel -- VERDICT r05 item 4, tools/diag_headline.py) and c3 (a
     # whole number of rotations per graph: a 64-B batch's kernel is ~9 us).
-    use_graph = args.graph == "on" or (args.graph == "auto" and args.config in ("c2", "c3"))
-    T = Timer(W, dev, use_graph, rotate=K,
-              exact_steps=args.steps if args.config == "c2" else 0)
+    # (c2 over K > 1 rotating batches -- a reduced --packets -- keeps stream
+    # launches: a graph of exactly K' < K steps would leave batches its
+    # replays never launch, and every batch's results are checked)
+    c2_graph = args.config == "c2" and K == 1
+    use_graph = args.graph == "on" or (args.graph == "auto" and (args.config == "c3" or c2_graph))
+    T = Timer(W, dev, use_graph, rotate=K, exact_steps=args.steps if c2_graph else 0)
     T.warm(args.warmup, args.warmup_seconds)
     wdist.barrier(dev)
 
@@ -1024,15 +1029,26 @@ def main():
     stream = torch.cuda.current_stream(dev)  # the stream every launch goes to
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
+    # Every rank leaves the barrier together (t0), times its own K steps until
+    # its device has finished them (synchronize), and the slowest rank's time
+    # is the job's (max over ranks); the closing barrier aligns the ranks
+    # again outside the timed region, so its collective's own latency is not
+    # counted as checksum time.
     gc.disable()  # (no collector pass inside the timed region)
     t0 = time.perf_counter()
     ev0.record(stream)
     T.run(steps)
     ev1.record(stream)
-    wdist.barrier(dev)
+    torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     gc.enable()
+    wdist.barrier(dev)
     kernel_ms = ev0.elapsed_time(ev1) / steps
+    timing = ((f"hipGraph replay ({T.per_graph} launches per graph)" if use_graph
+               else "stream launches")
+              + "; whole-job time: from a barrier + synchronize to this rank's "
+                "synchronize, max over ranks; kernel time from HIP events on the launch "
+                "stream")
 
     elapsed = wdist.max_over_ranks(elapsed, coll_dev)
     kernel_ms_max = wdist.max_over_ranks(kernel_ms, coll_dev)
@@ -1114,10 +1130,7 @@ def main():
                 "frac_job": round(frac_job, 4),
                 "kernel_ms_avg": round(kernel_ms, 5),
                 "kernel_ms_avg_max_rank": round(kernel_ms_max, 5),
-                "timing": ((f"hipGraph replay ({T.per_graph} launches per graph)"
-                            if use_graph else "stream launches")
-                           + "; whole-job time from barrier + synchronize to barrier + "
-                             "synchronize, kernel time from HIP events on the launch stream")}
+                "timing": timing}
         if frac_l3 is not None:
             roof["frac_l3_resident"] = frac_l3
         if c2rot is not None:

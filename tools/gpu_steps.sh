@@ -13,7 +13,8 @@
 #   bench_args    bench.py $BENCH_ARGS (> bench_args.json)
 #   prof_c2       rocprofv3 --kernel-trace --stats of the driver's headline command
 #   diag_headline tools/diag_headline.py (the headline's whole-job gap, by issue mode)
-#   tune          tools/tune.py $TUNE_ARGS (> tune.log)
+#   tune          tools/tune.py once per '|'-separated argument set in $TUNE_ARGS
+#                 (> tune1.log, tune2.log, ...; quote --variants specs inside)
 #   e2e           tools/e2e.py $E2E_ARGS (host-path variants, end to end)
 #   ab            A/B of WC_LIB=$AB_LIB against the in-tree library, tune.py $AB_ARGS
 #                 (';'-separated cases), $AB_REPS alternating rounds
@@ -31,10 +32,11 @@ export TMPDIR=/tmp WC_NO_BUILD=1
 step() {  # $1 = name, $2 = seconds, rest = command; stdout/stderr -> $OUT/$1.log
     local name=$1 secs=$2; shift 2
     echo "== $name ($(date +%T))"
+    local t0=$SECONDS
     timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
     local rc=$?
     tail -4 "$OUT/$name.log"
-    echo "$name rc=$rc" >> "$OUT/summary.log"
+    echo "$name rc=$rc wall_s=$((SECONDS - t0))" >> "$OUT/summary.log"
     if [ $rc -ne 0 ]; then
         echo "step $name ended with $rc: stopping"
         exit $rc
@@ -63,7 +65,12 @@ for s in ${STEPS:-pytest smoke bench}; do
         diag_headline)
             step diag_headline 300 python tools/diag_headline.py --json "$OUT/diag_headline.json" ;;
         tune)
-            step tune 600 python tools/tune.py ${TUNE_ARGS:-} ;;
+            IFS='|' read -ra runs <<< "${TUNE_ARGS:-}"
+            k=0
+            for a in "${runs[@]}"; do
+                k=$((k + 1))
+                eval "step tune$k 600 python tools/tune.py $a"
+            done ;;
         e2e)
             step e2e 500 python tools/e2e.py ${E2E_ARGS:-} ;;
         ab)

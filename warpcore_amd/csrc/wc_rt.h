@@ -329,8 +329,12 @@ int out_size(int kind);
 int host_zero_copy(Device &D, const uint8_t *dbase, const uint64_t *h_off,
                    const uint16_t *h_len, uint64_t n, uint8_t *h_out, int kind,
                    uint16_t *h_out2 = nullptr);
+// Every packet of a host batch inside [0, h_bytes); whether the offsets
+// ascend, the bytes the packets' checks read, and (optional) the byte range
+// they span.
 bool host_batch_ok(const uint8_t *hb, uint64_t h_bytes, const uint64_t *h_off,
-                   const uint16_t *h_len, uint64_t n, int kind, bool *ascending, uint64_t *total);
+                   const uint16_t *h_len, uint64_t n, int kind, bool *ascending, uint64_t *total,
+                   uint64_t *range = nullptr);
 void shard_range(uint64_t n, int g, int G, uint64_t *lo, uint64_t *hi);
 
 // Pipelined path over one HostPipe on one device (wc_rt_host.cpp): one chunk
