@@ -135,13 +135,17 @@ int wc_rx_verdict_host(const void *h_base, uint64_t h_bytes, const uint64_t *h_o
 /* Same as wc_cksum_ragged, but every buffer is host memory: packet i is
  * h_len[i] bytes at h_base + h_off[i], inside [h_base, h_base + h_bytes)
  * (WC_EINVAL otherwise), in any order.  Synchronous; results land in h_out.
- *   - Registered region (wc_host_register), small batch (<= 4096 packets,
- *     <= 8 MiB; WC_ZC_BYTES overrides): one kernel reads the packets in
- *     place over PCIe -- the low-latency path for a socket or ring batch.
+ *   - Registered region (wc_host_register), up to 256 packets: the resident
+ *     server grid answers (no launch); up to 4096 packets and 8 MiB: one
+ *     kernel reads the packets in place over PCIe -- the low-latency path for
+ *     a socket or ring batch.
+ *   - Registered, larger, and sparse (the packets cover < 7/8 of their byte
+ *     range: netmap slots) or out of order: kernels read the packets in place,
+ *     64 K packets per launch -- only the lines they touch cross the link.
  *   - Otherwise chunks are streamed over several HIP streams with
- *     hipMemcpyAsync: ascending offsets ship the byte range a chunk covers
- *     (DMA straight from a registered region), any other order is gathered
- *     into the library's pinned staging first. */
+ *     hipMemcpyAsync: dense ascending offsets ship the byte range a chunk
+ *     covers (DMA straight from a registered region), anything else is
+ *     gathered packet by packet into the library's pinned staging first. */
 int wc_cksum_host(const void *h_base, uint64_t h_bytes, const uint64_t *h_off,
                   const uint16_t *h_len, uint64_t n, uint16_t *h_out, int kind);
 
