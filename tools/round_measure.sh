@@ -39,5 +39,5 @@ for c in ${CFGS:-c2 c4 c4pl slotspl}; do
         2> gpurun_out/round/bench_${TAG}_$c.err || { tail gpurun_out/round/bench_${TAG}_$c.err; exit 1; }
     cat gpurun_out/round/bench_${TAG}_$c.json
     echo "== $c: rocprof"
-    TAG=${TAG}_$c BENCH_ARGS="$a --steps 50 --warmup 5 --no-cpu-baseline --no-c5 --no-extra --graph off" tools/profile.sh || exit 1
+    TAG=${TAG}_$c BENCH_ARGS="$a --steps 50 --warmup 5 --no-cpu-baseline --no-c5 --no-extra --no-e2e --graph off" tools/profile.sh || exit 1
 done
