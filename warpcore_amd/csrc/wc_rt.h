@@ -170,6 +170,7 @@ struct Config {
     int zc_group_max = (int)kZcGroupMax; // WC_ZC_GROUP_MAX
     int zc_bytes = kZcBytesDefault;      // WC_ZC_BYTES
     int zc_stream = 1;             // WC_ZC_STREAM: large registered batches read in place (0: pipeline)
+    uint64_t zs_pkts = kZsPkts;    // WC_ZS_PKTS: packets per zero-copy stream launch (<= kZsPkts)
     uint64_t flat_min = kFlatMinDefault; // WC_FLAT_MIN: ragged group kernel below this n
     int diag_noload = 0;           // WC_DIAG_NOLOAD: timing-only kernel (tuning build)
     int nt = 1;                    // WC_NT: nontemporal loads

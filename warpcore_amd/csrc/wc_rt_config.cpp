@@ -88,6 +88,7 @@ void load_config_locked()
     c.zc_group_max = env_int("WC_ZC_GROUP_MAX", c.zc_group_max);
     c.zc_bytes = env_int("WC_ZC_BYTES", c.zc_bytes);
     c.zc_stream = env_int("WC_ZC_STREAM", c.zc_stream);
+    c.zs_pkts = std::max<uint64_t>(1024, std::min<uint64_t>(env_u64("WC_ZS_PKTS", c.zs_pkts), kZsPkts));
     c.flat_min = env_u64("WC_FLAT_MIN", c.flat_min);
     c.nt = env_int("WC_NT", c.nt);
     c.grp_dense = env_int("WC_GRP_DENSE", c.grp_dense);

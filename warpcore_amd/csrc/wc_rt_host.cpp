@@ -251,8 +251,9 @@ int host_zc_stream(Device &D, const uint8_t *dbase, const uint64_t *h_off,
         return WC_OK;
     };
     int b = 0;
-    for (uint64_t i = 0; i < n && rc == WC_OK; i += kZsPkts, b ^= 1) {
-        const uint64_t cnt = std::min(kZsPkts, n - i);
+    const uint64_t per = g_cfg.zs_pkts;
+    for (uint64_t i = 0; i < n && rc == WC_OK; i += per, b ^= 1) {
+        const uint64_t cnt = std::min(per, n - i);
         rc = drain(b); // (chunk k - 2's results: its buffers are free again)
         if (rc)
             break;
