@@ -264,9 +264,12 @@ int wc_gpu_init(int device);
  * the caller quiesces its engine threads first. */
 int wc_gpu_fini(void);
 
-/* The WC_* tuning environment (kernel shapes, path choices) is
- * read once, at the first initialisation.  Re-read it now (A/B tuning tools
- * and tests; never needed in production). */
+/* The WC_* environment is read once, at the first initialisation.  This
+ * (shipped) library reads only the resident server's WC_SERVE (0: off),
+ * WC_SERVE_IDLE_US, WC_SERVE_WAVES and WC_SERVE_MAX, and the staging pool's
+ * WC_STAGE_THREADS; its kernel shapes and path choices are a compile-time
+ * table.  The tuning build (libwccksum_tune.so, -DWC_TUNING) also reads every
+ * path knob.  Re-read the environment now. */
 int wc_config_reload(void);
 
 /* Counter-based synthetic packet bytes (bench / tests): little-endian 8-byte
