@@ -130,7 +130,7 @@ def parse(argv=None):
                     help="skip the end-to-end (host memory in and out) object")
     ap.add_argument("--e2e-packets", type=int, default=1 << 20,
                     help="packets per rank of each end-to-end call")
-    ap.add_argument("--e2e-reps", type=int, default=3, help="timed calls per e2e case")
+    ap.add_argument("--e2e-reps", type=int, default=5, help="timed calls per e2e case")
     ap.add_argument("--traffic-file", default=str(ROOT / "profiles" / "traffic.json"))
     return ap.parse_args(argv)
 

@@ -16,7 +16,10 @@
  *     that stream only;
  *   - a scalar caller: the drop-in ip_cksum / payload_cksum;
  *   - a churn thread: registers and unregisters a scratch region over and
- *     over (each stops the resident server grid) and reads the server stats.
+ *     over (each stops the resident server grid) and reads the server stats;
+ *   - a pauser: wc_server_pause, then a device-wide hipDeviceSynchronize
+ *     while the host engines keep calling (it must return within 0.5 s:
+ *     no grid left to wait for), then wc_server_resume, every ~40 ms.
  * Every result is compared with the oracle (oracle/wc_oracle.c) on the same
  * bytes.  At the end the server must have answered and never failed
  * (wc_server_stats: served > 0, fallbacks 0).
@@ -387,6 +390,45 @@ static void *churn(void *p)
     return NULL;
 }
 
+/* The quiesce API under traffic: after wc_server_pause no grid is resident,
+ * so a device-wide synchronisation waits only for the engines' own short
+ * kernels -- never for the next idle period of the host engines. */
+static double g_max_sync_s = 0;
+
+static void *pauser(void *p)
+{
+    struct result *r = p;
+    const double t_end = now_s() + g_seconds;
+    while (!g_stop && now_s() < t_end) {
+        if (wc_server_pause() != WC_OK) {
+            fprintf(stderr, "pauser: wc_server_pause failed\n");
+            r->bad++;
+            break;
+        }
+        const double t0 = now_s();
+        const hipError_t e = hipDeviceSynchronize();
+        const double dt = now_s() - t0;
+        if (dt > g_max_sync_s)
+            g_max_sync_s = dt;
+        if (e != hipSuccess || dt > 0.5) {
+            fprintf(stderr, "pauser: device sync after a pause took %.3f s (%s)\n", dt,
+                    hipGetErrorString(e));
+            r->bad++;
+        }
+        struct timespec ts = {0, 10 * 1000 * 1000}; /* 10 ms paused */
+        nanosleep(&ts, NULL);
+        if (wc_server_resume() != WC_OK) {
+            fprintf(stderr, "pauser: wc_server_resume failed\n");
+            r->bad++;
+            break;
+        }
+        r->calls++;
+        ts.tv_nsec = 30 * 1000 * 1000; /* 30 ms serving */
+        nanosleep(&ts, NULL);
+    }
+    return NULL;
+}
+
 /* Every engine must have been served in turn: the library's lock is first
  * come, first served, and device-resident calls do not wait for it. */
 static int starved(const char *who, int id, uint64_t calls, uint64_t min_calls)
@@ -432,7 +474,7 @@ int main(int argc, char **argv)
     pthread_t th[32];
     struct host_arg ha[16];
     struct dev_arg da[8];
-    struct result sc = {0}, ch = {0};
+    struct result sc = {0}, ch = {0}, pz = {0};
     int k = 0;
     for (int i = 0; i < nh; ++i) {
         ha[i] = (struct host_arg){i, i % 4 != 3, {0}}; /* every 4th region pageable */
@@ -444,10 +486,11 @@ int main(int argc, char **argv)
     }
     pthread_create(&th[k++], NULL, scalar_caller, &sc);
     pthread_create(&th[k++], NULL, churn, &ch);
+    pthread_create(&th[k++], NULL, pauser, &pz);
     for (int i = 0; i < k; ++i)
         pthread_join(th[i], NULL);
 
-    uint64_t bad = sc.bad + ch.bad;
+    uint64_t bad = sc.bad + ch.bad + pz.bad;
     printf("thread_engines: %.1f s, %d host engines, %d device engines\n", g_seconds, nh, nd);
     for (int i = 0; i < nh; ++i) {
         printf("  host %d (%s): %llu calls, %llu packets, %llu mismatches\n", i,
@@ -464,7 +507,10 @@ int main(int argc, char **argv)
     printf("  scalar: %llu calls, %llu mismatches; churn: %llu register cycles\n",
            (unsigned long long)sc.calls, (unsigned long long)sc.bad,
            (unsigned long long)ch.calls);
-    bad += starved("scalar", 0, sc.calls, 20) + starved("churn", 0, ch.calls, 5);
+    printf("  pauser: %llu pause / sync / resume cycles, longest device sync %.1f ms\n",
+           (unsigned long long)pz.calls, g_max_sync_s * 1e3);
+    bad += starved("scalar", 0, sc.calls, 20) + starved("churn", 0, ch.calls, 5) +
+           starved("pauser", 0, pz.calls, 5);
     uint64_t served = 0, fb = 0, l = 0;
     wc_server_stats(&served, &fb, &l);
     printf("  server: %llu batches served, %llu fallbacks, %llu grid launches\n",

@@ -217,9 +217,11 @@ def test_c_thread_engines(gpu, tmp_path):
     (tests/c/thread_engines.c): host engines over registered and pageable
     buffer regions (server, zero-copy, pipeline; ip / payload / fused / RX
     verdicts), device engines on their own streams (strided / ragged / fused /
-    RX), the scalar drop-in, and a thread that keeps registering and
-    unregistering a region (each stops the server grid).  Every result equals
-    the oracle's, and the server answered with no fallback."""
+    RX), the scalar drop-in, a thread that keeps registering and
+    unregistering a region (each stops the server grid), and one that keeps
+    pausing the server, synchronising the whole device (bounded: no grid
+    left) and resuming it.  Every result equals the oracle's, and the server
+    answered with no fallback."""
     import subprocess
 
     from cprog import build
