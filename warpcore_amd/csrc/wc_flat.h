@@ -302,6 +302,7 @@ __device__ __forceinline__ uint16_t lane_hdr_cksum(uint64_t a, uint32_t hl,
 // PK (q - cp) + j, at vb + 16 (PK q + j).
 struct FlatTile {
     uint32_t cp, ce, total, rank, last_rank;
+    uint32_t ends; // ce - 1 if another non-empty packet follows this one, else ~0 (GathSrc)
 };
 
 template <int UN, int PK, bool VSUM = false>
@@ -329,6 +330,7 @@ __device__ __forceinline__ FlatTile flat_tile_setup(FlatLds<UN> &L, int lane, ui
     const uint64_t nonempty = __ballot(nch != 0);
     t.rank = mbcnt64(nonempty);
     t.last_rank = nonempty ? (uint32_t)__builtin_popcountll(nonempty) - 1u : 0u;
+    t.ends = nch != 0 && t.rank < t.last_rank ? t.ce - 1u : 0xFFFFFFFFu;
     const uint64_t vb = (a & ~15ull) - 16ull * PK * t.cp;
     if (nch != 0)
         L.desc[t.rank] = FlatDesc{(uint32_t)vb, (uint32_t)(vb >> 32), s + 16u * PK * t.cp, info};

@@ -28,6 +28,23 @@
 // WC_RX_TRUNCATED.  Roofline: HBM, the checked frames' bytes once.
 #include "wc_seg.h"
 
+#ifdef WC_DIAG_STAMPS
+// Timing diagnostic build only (tools/rx_stamps.py): per tile, lane 0 stores
+// the 100-MHz wall clock at phase boundaries, the wave's hardware ids and the
+// tile's stream length.
+constexpr uint64_t kStampTiles = 1u << 16;
+__device__ uint32_t g_rx_stamps[kStampTiles * 8];
+#define WC_STAMP(k, v)                                                         \
+    do {                                                                       \
+        if (lane == 0 && tile < kStampTiles)                                   \
+            g_rx_stamps[tile * 8 + (k)] = (v);                                 \
+    } while (0)
+#define WC_CLOCK() ((uint32_t)wall_clock64())
+#else
+#define WC_STAMP(k, v) ((void)0)
+#define WC_CLOCK() 0u
+#endif
+
 namespace wc {
 namespace {
 
@@ -358,6 +375,7 @@ k_rx_verdict(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
     meta_load(offs, flens, tile * 64 + lane, n, off_n, flen_n);
 
     for (; tile < ntiles; tile += nwaves) {
+        WC_STAMP(0, WC_CLOCK());
         const uint64_t p = tile * 64 + lane;
         const bool valid = p < n;
         const uint64_t fa = (uint64_t)base + off_n;
@@ -370,6 +388,13 @@ k_rx_verdict(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
             rx_load_t(fa, flen, valid, zero, lane, reinterpret_cast<u32x4 *>(L.f.desc), hx, c4);
         else
             rx_load(fa, flen, valid, zero, c);
+        WC_STAMP(1, WC_CLOCK());
+#ifdef WC_DIAG_STAMPS
+        if (lane == 0 && tile < kStampTiles) {
+            g_rx_stamps[tile * 8 + 6] = __builtin_amdgcn_s_getreg(4 | (31 << 11));  // HW_ID
+            g_rx_stamps[tile * 8 + 7] = __builtin_amdgcn_s_getreg(20 | (15 << 11)); // XCC_ID
+        }
+#endif
         auto headers = [&] { // this lane's frame chunks 0..4 (HT: through LDS)
             if constexpr (HT)
                 rx_hdr_gather(L.stage, lane, hx, c4, c);
@@ -415,6 +440,7 @@ k_rx_verdict(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
                     need = h.need && !slow;
                     on = need;
                     len = need ? h.plen : 0u;
+                    WC_STAMP(2, WC_CLOCK() | (uint32_t)(h.verdict & 0u));
                     if constexpr (SKIP) {
                         if (spec && !need) // its later chunks: the zero chunk
                             L.f.desc[t.rank].info = 1u << 31;
@@ -426,6 +452,11 @@ k_rx_verdict(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
                 uint16_t r = seg_tile<UNS, WC_KIND_PAYLOAD, NT, false, Src, true, decltype(late)>(
                     L.f.pre, L.stage, L.pm, lane, ip, 16ull * t.cp + (ip & 15u), room, spec,
                     t.total, Src{&L.f, t}, zero, done, rh, late);
+                WC_STAMP(3, WC_CLOCK() | (uint32_t)(r & 0u));
+                WC_STAMP(5, t.total);
+#ifdef WC_DIAG_STREAM_NOLOAD
+                done = true; // (timing only: the stream's chunks are synthetic)
+#endif
                 if (need && !done) // header longer than the packet, or a possible wrap
                     r = lane_payload_exact<NT>(ip, h.plen);
                 v = h.verdict;
@@ -458,6 +489,7 @@ k_rx_verdict(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
         if (valid)
             verdict[p] = (uint8_t)v;
         ndrop += valid && rx_is_drop(v);
+        WC_STAMP(4, WC_CLOCK());
     }
     if (drops) {
         ndrop = group_sum<64>(ndrop);
@@ -524,3 +556,13 @@ hipError_t launch_rx_verdict(const void *base, const uint64_t *offs, const uint1
 }
 
 } // namespace wc
+
+#ifdef WC_DIAG_STAMPS
+extern "C" int wc_diag_rx_stamps(uint32_t *host, uint64_t words)
+{
+    if (words > kStampTiles * 8)
+        words = kStampTiles * 8;
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_rx_stamps), words * 4, 0,
+                                    hipMemcpyDeviceToHost);
+}
+#endif

@@ -272,6 +272,17 @@ struct DenseSrc {
     }
 };
 
+//
+// GathSrc's owner lookup ("end bits"): slot s belongs to the packet of rank
+// = the number of packets whose last slot lies before s (counting only
+// packets followed by another non-empty one, FlatTile::ends, so the count
+// stops at the last rank for slots past the tile's end).  Per row group,
+// each such packet whose last slot falls in the group sets that slot's bit
+// in a 64-bit word per row (one LDS OR per packet lane); per row, the count
+// is a ballot of the packets that ended before the row plus an mbcnt of the
+// row's word below the lane.  The per-row run-start marks of flat_issue
+// (a row-tagged store, two ballots, readlane and mbcnt per row) took about
+// 16 VALU and 10 SALU per row; this takes about 4.
 template <int UNS, bool NT, bool SKIP = false>
 struct GathSrc {
     static constexpr bool kClamp = true;
@@ -279,12 +290,44 @@ struct GathSrc {
     FlatTile t;
     __device__ __forceinline__ void issue(SegRows<UNS> &R, uint32_t g0, int lane) const
     {
-        FlatRows<UNS, 1> F;
-        flat_issue<UNS, NT, false, 1, WC_KIND_IP, SKIP>(F, *L, g0, lane, t.cp, t.ce, t.rank,
-                                                        t.last_rank, t.total);
+        constexpr uint32_t kGrp = 64u * UNS;
+        uint64_t *M = reinterpret_cast<uint64_t *>(&L->mark[0][0]); // one word per row
+        wave_order(); // (after the previous group's reads)
+        if (lane < UNS) {
+            uint32_t z0, z1; // materialised here, not hoisted into registers held across the tile
+            asm volatile("v_mov_b32 %0, 0\n\tv_mov_b32 %1, 0" : "=v"(z0), "=v"(z1));
+            M[lane] = (uint64_t)z0 | ((uint64_t)z1 << 32);
+        }
+        wave_order();
+        const uint32_t d = t.ends - g0; // (~0 - g0: never below kGrp)
+        if (d < kGrp)
+            __hip_atomic_fetch_or(&M[d >> 6], 1ull << (d & 63u), __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_WORKGROUP);
+        wave_order();
 #pragma unroll
-        for (int u = 0; u < UNS; ++u)
-            R.d[u] = F.d[u][0];
+        for (int u = 0; u < UNS; ++u) {
+            const uint64_t m = M[u]; // the same address in every lane: a broadcast read
+            const uint32_t row0 = g0 + 64u * u;
+            const uint32_t before = (uint32_t)__builtin_popcountll(__ballot(t.ends < row0));
+            const uint32_t own = __builtin_amdgcn_mbcnt_hi(
+                (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, before));
+            // Slots past the tile's end re-read its last chunk (zeroed in
+            // seg_accum): a straight-line issue stream.
+            const uint32_t q = min(row0 + (uint32_t)lane, t.total - 1u);
+            if constexpr (SKIP) {
+                const FlatDesc g = L->desc[own];
+                const uint64_t vb = (uint64_t)g.vb_lo | ((uint64_t)g.vb_hi << 32);
+                R.d[u] = load_chunk<NT>((g.info >> 31) ? (uint64_t)(uintptr_t)&kZeroChunk
+                                                       : vb + 16ull * q);
+            } else {
+                const uint64_t vb = *reinterpret_cast<const uint64_t *>(&L->desc[own]);
+#ifdef WC_DIAG_STREAM_NOLOAD
+                R.d[u] = u32x4{(uint32_t)vb, q, (uint32_t)(vb >> 32), q ^ 0x5a5a5a5au};
+#else
+                R.d[u] = load_chunk<NT>(vb + 16ull * q);
+#endif
+            }
+        }
     }
 };
 
