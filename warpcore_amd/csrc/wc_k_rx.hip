@@ -345,8 +345,14 @@ __device__ __forceinline__ RxParse rx_parse_slow(uint64_t fa, uint32_t flen, boo
 // (4 waves per SIMD for every mode: capping the EARLY kernels at 96 VGPRs
 // for 5 spilled 4 of them and took the mixed ring from 114 to 141 us,
 // profiles/ab_r04_rx_early_waves.log.)
+// One-wave workgroups: a wave's slot is handed to the next tile as soon as
+// its own tile is done, not when the slowest of four is (mixed-size ring with
+// ARP frames 91.8 -> 89.1 us, the others unchanged: profiles/ab_r06m_rx_waves.log).
+constexpr int kRxWaves = 1;
+constexpr int kRxSpan = 15; // XCD super-blocks of 2^15 tiles, as the seg kernel's
+
 template <bool NT, bool EARLY, bool HT, bool SKIP, bool TALLY = false>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
+__global__ void __launch_bounds__(64 * kRxWaves) __attribute__((amdgpu_waves_per_eu(4)))
 k_rx_verdict(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs,
              const uint16_t *__restrict__ flens, uint64_t n, uint8_t *__restrict__ verdict,
              unsigned long long *__restrict__ drops, uint32_t *__restrict__ tally, uint32_t gen)
@@ -358,15 +364,15 @@ k_rx_verdict(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
         u32x4 stage[64 * UNS]; // also the header chunks' transpose (HT)
         u32x4 pm[17]; // seg_head's masks
     };
-    __shared__ Lds lds_all[kFlatWaves];
+    __shared__ Lds lds_all[kRxWaves];
 
     const int lane = threadIdx.x & 63;
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); // wave-uniform: SGPR
+    const int w = kRxWaves == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     Lds &L = lds_all[w];
     seg_init_masks(L.pm, lane); // read after the first row group's wave_order
     const uint64_t ntiles = (n + 63) / 64;
-    const uint64_t nwaves = (uint64_t)gridDim.x * kFlatWaves;
-    uint64_t tile = xcd_block(13 << 8) * kFlatWaves + w; // the seg kernel's XCD span
+    const uint64_t nwaves = (uint64_t)gridDim.x * kRxWaves;
+    uint64_t tile = xcd_block(kRxSpan << 8) * kRxWaves + w; // the seg kernel's XCD span
     uint32_t ndrop = 0;
     const uint64_t zero = (uint64_t)(uintptr_t)&kZeroChunk;
 
@@ -505,7 +511,7 @@ static hipError_t launch_rx_one(const void *base, const uint64_t *offs, const ui
                                 uint64_t n, uint8_t *verdict, uint64_t *drops, int grid,
                                 hipStream_t st, uint32_t *tally, uint32_t gen)
 {
-    hipLaunchKernelGGL((k_rx_verdict<NT, EARLY, HT, SKIP, TALLY>), dim3(grid), dim3(256), 0, st,
+    hipLaunchKernelGGL((k_rx_verdict<NT, EARLY, HT, SKIP, TALLY>), dim3(grid), dim3(64 * kRxWaves), 0, st,
                        (const uint8_t *)base, offs, flens, n, verdict,
                        (unsigned long long *)drops, tally, gen);
     return hipGetLastError();
@@ -522,7 +528,7 @@ hipError_t launch_rx_verdict(const void *base, const uint64_t *offs, const uint1
     // prefetched.
     const uint64_t cap = max_grid > 0 ? (uint64_t)max_grid : kMaxGridBlocks;
     const int grid = (int)std::min<uint64_t>(
-        cap, std::max<uint64_t>(1, (tiles + kFlatWaves - 1) / kFlatWaves));
+        cap, std::max<uint64_t>(1, (tiles + kRxWaves - 1) / kRxWaves));
     // EARLY streams only the checked frames: SKIP has nothing to skip there,
     // and is dropped so that NT and HDRT are still honoured.
     const bool early = mode & kRxEarly, ht = mode & kRxHdrT, skip = (mode & kRxSkip) && !early;
