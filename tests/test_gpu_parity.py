@@ -49,12 +49,18 @@ RAGGED_MODES = {
     "grp": {"WC_SEG": "1", "WC_GRP_DENSE": "0", "WC_GRP_SPARSE": "0"},
     "segflat": {"WC_SEG": "1", "WC_GATHER": "0"},
     "gath": {"WC_SEG": "1", "WC_GATHER": "2", "WC_GRP_DENSE": "65", "WC_GRP_SPARSE": "65"},
+    # the gathered stream's end-bit owner lookup with 2- and 8-row groups
+    "gath2": {"WC_SEG": "1", "WC_GATHER": "2", "WC_GRP_DENSE": "65", "WC_GRP_SPARSE": "65",
+              "WC_SEG_ROWS": "2"},
+    "gath8": {"WC_SEG": "1", "WC_GATHER": "2", "WC_GRP_DENSE": "65", "WC_GRP_SPARSE": "65",
+              "WC_SEG_ROWS": "8"},
     "default": {},
 }
 
 
 def ragged_mode(monkeypatch, mode: str) -> None:
-    for k in ("WC_SEG", "WC_GRP_DENSE", "WC_GRP_SPARSE", "WC_FLAT_PK", "WC_VARIANT", "WC_GATHER"):
+    for k in ("WC_SEG", "WC_GRP_DENSE", "WC_GRP_SPARSE", "WC_FLAT_PK", "WC_VARIANT", "WC_GATHER",
+              "WC_SEG_ROWS"):
         monkeypatch.delenv(k, raising=False)
     for k, v in RAGGED_MODES[mode].items():
         monkeypatch.setenv(k, v)
