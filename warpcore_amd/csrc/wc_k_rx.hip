@@ -460,9 +460,6 @@ k_rx_verdict(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
                     t.total, Src{&L.f, t}, zero, done, rh, late);
                 WC_STAMP(3, WC_CLOCK() | (uint32_t)(r & 0u));
                 WC_STAMP(5, t.total);
-#ifdef WC_DIAG_STREAM_NOLOAD
-                done = true; // (timing only: the stream's chunks are synthetic)
-#endif
                 if (need && !done) // header longer than the packet, or a possible wrap
                     r = lane_payload_exact<NT>(ip, h.plen);
                 v = h.verdict;
