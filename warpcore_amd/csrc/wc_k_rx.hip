@@ -30,8 +30,9 @@
 
 #ifdef WC_DIAG_STAMPS
 // Timing diagnostic build only (tools/rx_stamps.py): per tile, lane 0 stores
-// the 100-MHz wall clock at phase boundaries, the wave's hardware ids and the
-// tile's stream length.
+// the 100-MHz wall clock (s_memrealtime, which hipcc keeps in program order
+// with the loads and stores around it) at phase boundaries, the wave's
+// hardware ids and the tile's stream length.
 constexpr uint64_t kStampTiles = 1u << 16;
 __device__ uint32_t g_rx_stamps[kStampTiles * 8];
 #define WC_STAMP(k, v)                                                         \
@@ -446,7 +447,7 @@ k_rx_verdict(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
                     need = h.need && !slow;
                     on = need;
                     len = need ? h.plen : 0u;
-                    WC_STAMP(2, WC_CLOCK() | (uint32_t)(h.verdict & 0u));
+                    WC_STAMP(2, WC_CLOCK());
                     if constexpr (SKIP) {
                         if (spec && !need) // its later chunks: the zero chunk
                             L.f.desc[t.rank].info = 1u << 31;
@@ -458,7 +459,7 @@ k_rx_verdict(const uint8_t *__restrict__ base, const uint64_t *__restrict__ offs
                 uint16_t r = seg_tile<UNS, WC_KIND_PAYLOAD, NT, false, Src, true, decltype(late)>(
                     L.f.pre, L.stage, L.pm, lane, ip, 16ull * t.cp + (ip & 15u), room, spec,
                     t.total, Src{&L.f, t}, zero, done, rh, late);
-                WC_STAMP(3, WC_CLOCK() | (uint32_t)(r & 0u));
+                WC_STAMP(3, WC_CLOCK());
                 WC_STAMP(5, t.total);
                 if (need && !done) // header longer than the packet, or a possible wrap
                     r = lane_payload_exact<NT>(ip, h.plen);
