@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Does the host NUMA node of a batch's pages set the end-to-end rate?
 
-    python tools/numa_probe.py [--reps 5]
+    python tools/numa_probe.py [--reps 5] [--align]
 
 Prints the GPU's NUMA node (sysfs, from its PCI bus id), this process's
 allowed CPUs per node, then for each node that has allowed CPUs: C2's bytes
@@ -97,5 +97,46 @@ def main() -> None:
               f"mismatches {bad}", flush=True)
 
 
+def align_probe(args) -> None:
+    """The same call with the batch's start at several offsets from a page
+    boundary (bench.py's batch is a torch CPU tensor, whose start is not
+    page-aligned), and from a torch CPU tensor as bench.py makes it."""
+    dev = torch.device("cuda:0")
+    n, L = args.packets, 1472
+    d = torch.empty(n * L, dtype=torch.uint8, device=dev)
+    wc.synth_fill(d, 7, nbytes=n * L)
+    src = d.cpu().numpy()
+    want = c_oracle.cksum_strided(src, L, L, n, kind=0)
+    off = np.arange(n, dtype=np.uint64) * np.uint64(L)
+    ln = np.full(n, L, dtype=np.uint16)
+    big = np.empty(n * L + 8192, dtype=np.uint8)
+    base = (-big.ctypes.data) % 4096
+    cases = [(f"page + {k}", big[base + k: base + k + n * L]) for k in (0, 16, 64, 256, 2048)]
+    cases.append((f"torch CPU tensor (start mod 4096 = {src.ctypes.data % 4096})", src))
+    for name, buf in cases:
+        if buf is not src:
+            buf[:] = src
+        wc.host_register(buf)
+        try:
+            bad = int((wc.cksum_host(buf, off, ln, kind="ip") != want).sum())
+            ts = []
+            for _ in range(args.reps):
+                t0 = time.perf_counter()
+                wc.cksum_host(buf, off, ln, kind="ip")
+                ts.append(time.perf_counter() - t0)
+        finally:
+            wc.host_unregister(buf)
+        print(f"{name}: wc_cksum_host registered {n * L / min(ts) / 1e9:.2f} GB/s, "
+              f"mismatches {bad}", flush=True)
+
+
 if __name__ == "__main__":
+    if "--align" in sys.argv:
+        sys.argv.remove("--align")
+        _ap = argparse.ArgumentParser()
+        _ap.add_argument("--reps", type=int, default=5)
+        _ap.add_argument("--packets", type=int, default=1 << 20)
+        wc.gpu_init(0)
+        align_probe(_ap.parse_args())
+        sys.exit(0)
     main()
