@@ -113,9 +113,17 @@ def align_probe(args) -> None:
     base = (-big.ctypes.data) % 4096
     cases = [(f"page + {k}", big[base + k: base + k + n * L]) for k in (0, 16, 64, 256, 2048)]
     cases.append((f"torch CPU tensor (start mod 4096 = {src.ctypes.data % 4096})", src))
+    cases.append(("the tensor again, after a torch H2D copy from it while registered", src))
     for name, buf in cases:
         if buf is not src:
             buf[:] = src
+        if name.startswith("the tensor again"):
+            # bench.py's e2e leg: the copy ceiling registers the batch, copies
+            # it with torch, unregisters it; then the calls register it again
+            wc.host_register(buf)
+            d.copy_(torch.from_numpy(buf), non_blocking=True)
+            torch.cuda.synchronize()
+            wc.host_unregister(buf)
         wc.host_register(buf)
         try:
             bad = int((wc.cksum_host(buf, off, ln, kind="ip") != want).sum())
