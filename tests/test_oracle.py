@@ -207,3 +207,32 @@ def test_rx_verdict_reference_details():
     # ARP and the rest go to the host (eth.c:75-86)
     arp = bytes(12) + b"\x08\x06" + bytes(28)
     assert v.rx_verdict(arp) == v.RX_NOT_IP == c_oracle.rx_verdict(arp)
+
+
+def test_oracle_build_is_safe_for_concurrent_ranks(tmp_path):
+    """The ranks of a multi-GPU bench start at once; on a host CPU model with
+    no oracle build yet, every rank builds it on first use.  Round 6 saw 8
+    gloo ranks collide on the same output file (`file too short`, a vanished
+    `.tmp`); warpcore_amd/_build.py now serializes the build with a lock and
+    gives each process its own temporary file.  Six processes build a fresh
+    tag's oracle at once, and every one of them loads it."""
+    import os
+    import shutil
+    import subprocess
+    import sys
+
+    root = Path(__file__).resolve().parent.parent
+    tag = f"racetest-{os.getpid()}"
+    code = ("import ctypes; from warpcore_amd import _build; "
+            "p = _build.build_oracle(); ctypes.CDLL(str(p)); print(p)")
+    env = dict(os.environ, WC_ORACLE_BUILD_TAG=tag, PYTHONPATH=str(root))
+    try:
+        procs = [subprocess.Popen([sys.executable, "-c", code], cwd=root, env=env,
+                                  stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+                 for _ in range(6)]
+        outs = [p.communicate(timeout=300) for p in procs]
+        for p, (out, err) in zip(procs, outs):
+            assert p.returncode == 0, err[-2000:]
+        assert len({o.strip() for o, _ in outs}) == 1
+    finally:
+        shutil.rmtree(root / "oracle" / f"build-{tag}", ignore_errors=True)

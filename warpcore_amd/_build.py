@@ -19,6 +19,8 @@ machine keeps its binary only if it was built from exactly these sources.
 """
 from __future__ import annotations
 
+import contextlib
+import fcntl
 import hashlib
 import os
 import platform
@@ -70,6 +72,22 @@ def _stamp(target: Path) -> Path:
     return target.with_name(target.name + ".srchash")
 
 
+@contextlib.contextmanager
+def _build_lock(target: Path):
+    """One builder per target across processes: the ranks of a multi-GPU run
+    start at once, and on a host whose CPU model has no oracle build yet every
+    rank would otherwise compile it into the same file (seen in round 6: 8
+    gloo ranks, `file too short` / a vanished `.tmp`).  The others wait, then
+    find it current."""
+    target.parent.mkdir(parents=True, exist_ok=True)
+    with open(target.parent / f".{target.name}.lock", "w") as lf:
+        fcntl.flock(lf, fcntl.LOCK_EX)
+        try:
+            yield
+        finally:
+            fcntl.flock(lf, fcntl.LOCK_UN)
+
+
 def _stale(target: Path, deps, flags) -> bool:
     st = _stamp(target)
     if not target.exists() or not st.exists():
@@ -96,6 +114,13 @@ def build_lib(force: bool = False, verbose: bool = False, tuning: bool = False) 
     target, flags = lib_path(tuning), lib_flags(tuning)
     if not force and not _stale(target, HIP_DEPS, flags):
         return target
+    with _build_lock(target):
+        if not force and not _stale(target, HIP_DEPS, flags):
+            return target  # another process built it while this one waited
+        return _build_lib_locked(target, flags, verbose)
+
+
+def _build_lib_locked(target: Path, flags, verbose: bool) -> Path:
     digest = _src_hash(HIP_DEPS, flags)
     with tempfile.TemporaryDirectory(prefix="wccksum-") as tmpdir:
         objs, procs = [], []
@@ -109,7 +134,7 @@ def build_lib(force: bool = False, verbose: bool = False, tuning: bool = False) 
         failed = [cmd for cmd, p in procs if p.wait() != 0]
         if failed:
             raise subprocess.CalledProcessError(1, failed[0])
-        tmp = target.with_suffix(".so.tmp")
+        tmp = target.with_name(f"{target.name}.{os.getpid()}.tmp")
         cmd = [_hipcc(), "--offload-arch=gfx950", "-fPIC", "-shared", "-o", str(tmp), *objs]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
@@ -132,7 +157,9 @@ def _cpu_tag() -> str:
 
 
 def oracle_path() -> Path:
-    return ORACLE_DIR / f"build-{_cpu_tag()}" / "libwc_oracle.so"
+    # WC_ORACLE_BUILD_TAG (tests only) names a build directory of its own
+    tag = os.environ.get("WC_ORACLE_BUILD_TAG") or _cpu_tag()
+    return ORACLE_DIR / f"build-{tag}" / "libwc_oracle.so"
 
 
 def build_oracle(force: bool = False, verbose: bool = False) -> Path:
@@ -140,14 +167,16 @@ def build_oracle(force: bool = False, verbose: bool = False) -> Path:
     out = oracle_path()
     if not force and not _stale(out, ORACLE_SOURCES, ["oracle"]):
         return out
-    out.parent.mkdir(parents=True, exist_ok=True)
-    tmp = out.with_suffix(".so.tmp")
-    cmd = ["make", "-s", "-C", str(ORACLE_DIR), f"OUT={tmp}", "oracle"]
-    if verbose:
-        print(" ".join(cmd), file=sys.stderr)
-    subprocess.run(cmd, check=True)
-    os.replace(tmp, out)
-    _stamp(out).write_text(_src_hash(ORACLE_SOURCES, ["oracle"]) + "\n")
+    with _build_lock(out):
+        if not force and not _stale(out, ORACLE_SOURCES, ["oracle"]):
+            return out  # another process built it while this one waited
+        tmp = out.with_name(f"{out.name}.{os.getpid()}.tmp")
+        cmd = ["make", "-s", "-C", str(ORACLE_DIR), f"OUT={tmp}", "oracle"]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+        os.replace(tmp, out)
+        _stamp(out).write_text(_src_hash(ORACLE_SOURCES, ["oracle"]) + "\n")
     return out
 
 
