@@ -81,11 +81,16 @@ def _build_lock(target: Path):
     find it current."""
     target.parent.mkdir(parents=True, exist_ok=True)
     with open(target.parent / f".{target.name}.lock", "w") as lf:
-        fcntl.flock(lf, fcntl.LOCK_EX)
+        try:
+            fcntl.flock(lf, fcntl.LOCK_EX)
+            locked = True
+        except OSError:  # a filesystem without flock: per-process temp files still apply
+            locked = False
         try:
             yield
         finally:
-            fcntl.flock(lf, fcntl.LOCK_UN)
+            if locked:
+                fcntl.flock(lf, fcntl.LOCK_UN)
 
 
 def _stale(target: Path, deps, flags) -> bool:
